@@ -1,0 +1,188 @@
+/*
+ * matvec_gpu.h — C-ABI of libmatvec_gpu.so, the MI355X (gfx950) replacement for the
+ * compute + communication core of yaroslav-i-am/MatVec_MPI_Multiplier.
+ *
+ * Plain C types only (pointers, int64_t sizes, int return codes). No torch, no HIP
+ * types in any signature: streams are passed as `void*` (a hipStream_t, NULL = the
+ * library's own stream for that device).
+ *
+ * Every function returns MVG_OK (0) on success or a negative MVG_E* code; the text of
+ * the last failure on the calling thread is available from mvg_last_error().
+ *
+ * Reference interfaces replaced (paths relative to the reference repository):
+ *   mvg_gemv                 <- multiply_std_rowwise          src/matr_utils.c:86-96
+ *                               (also the strip GEMV that multiply_colwise computes as
+ *                                scale-then-row-sum,          src/multiplier_colwise.c:105-122)
+ *   mvg_grid_shape           <- get_2_most_closest_multipliers src/utils.c:26-37
+ *   mvg_plan_shard           <- local_n / local_n_rows / local_n_cols arithmetic
+ *                               src/multiplier_rowwise.c:93, src/multiplier_colwise.c:349,
+ *                               src/multiplier_blockwise.c:299-306 (+ divisibility checks
+ *                               rowwise.c:72-75, colwise.c:151-154, blockwise.c:277-281)
+ *   mvg_engine_distribute    <- distribute_data (Scatter/Bcast | Type_vector+Pack+Send |
+ *                               block Pack+Send)  rowwise.c:12-51, colwise.c:11-102,
+ *                               blockwise.c:17-141
+ *   mvg_engine_multiply      <- local multiply + MPI_Gather / MPI_Reduce(SUM) /
+ *                               gather_local_results
+ *                               rowwise.c:140-141, colwise.c:105-129, blockwise.c:144-210,367-368
+ *   mvg_engine_collect       <- root owning `result` after the timed region (the reference
+ *                               never writes y; this is the opt-in y hand-back)
+ *   mvg_load_matr / mvg_load_vec <- load_matr / load_vec       src/matr_utils.c:42-83
+ *   mvg_comm_*               <- MPI_Init/Comm_size/Comm_rank/Finalize + the collectives
+ *                               (RCCL over xGMI instead of MPI)
+ */
+#ifndef MATVEC_GPU_H
+#define MATVEC_GPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status codes */
+#define MVG_OK              0
+#define MVG_E_INVALID      -1   /* bad argument (null pointer, negative size, ...)   */
+#define MVG_E_INDIVISIBLE  -2   /* shape does not split over the rank count          */
+#define MVG_E_HIP          -3   /* HIP runtime failure                                */
+#define MVG_E_RCCL         -4   /* RCCL failure                                       */
+#define MVG_E_IO           -5   /* file missing / unreadable                          */
+#define MVG_E_NOMEM        -6   /* host or device allocation failed                   */
+#define MVG_E_STATE        -7   /* call out of order (e.g. multiply before distribute)*/
+
+/* ------------------------------------------------------------------ algorithms   */
+#define MVG_ALG_ROWWISE    0    /* src/multiplier_rowwise.c   */
+#define MVG_ALG_COLWISE    1    /* src/multiplier_colwise.c   */
+#define MVG_ALG_BLOCKWISE  2    /* src/multiplier_blockwise.c */
+
+const char* mvg_version(void);
+const char* mvg_strerror(int code);
+const char* mvg_last_error(void);
+
+/* ------------------------------------------------------------------ planner (host only, no GPU)
+ * get_2_most_closest_multipliers (src/utils.c:26-37): rows = largest d <= floor(sqrt(p))
+ * with p % d == 0, cols = p / d.  p <= 0 -> MVG_E_INVALID. */
+int mvg_grid_shape(int64_t p, int* grid_rows, int* grid_cols);
+
+/* The slice of the global R x C problem that rank `rank` of `nranks` owns.
+ * row_off/col_off/n_rows/n_cols: the block of A (and col_off/n_cols: the x segment);
+ * y_off/y_len: the slice of y its partial result contributes to.
+ * grid_r/grid_c: rank's coordinate in the grid (row-split: (rank,0), col-split: (0,rank)).
+ * Returns MVG_E_INDIVISIBLE exactly where the reference prints "ERROR!!!", and also
+ * (deliberate deviation) where the reference would silently compute a
+ * wrong y: block-split with R % r != 0 or C % c != 0. */
+typedef struct mvg_shard {
+    int     alg, nranks, rank;
+    int     grid_rows, grid_cols, grid_r, grid_c;
+    int64_t R, C;
+    int64_t row_off, col_off, n_rows, n_cols;
+    int64_t y_off, y_len;
+} mvg_shard;
+int mvg_plan_shard(int alg, int64_t R, int64_t C, int nranks, int rank, mvg_shard* out);
+
+/* ------------------------------------------------------------------ synthetic inputs
+ * value(seed, idx) = (double)k / 10000.0, k = floor(splitmix64(s0 + idx*gamma) * 10000 / 2^64),
+ * s0 = splitmix64(seed), gamma = 0x9E3779B97F4A7C15. Every value is exactly what "%.4f" text
+ * of it parses back to (the reference's data format, README.md:32), so synthetic and text
+ * inputs are interchangeable bit for bit. A uses idx = i*C + j of the GLOBAL matrix; x uses
+ * its own seed.  The device fill writes a shard [row_off, +m) x [col_off, +k) of a global
+ * R x C matrix (n_cols_global = C) into dst with leading dimension ld. */
+#define MVG_SEED_A 42u
+#define MVG_SEED_X 4242u
+double mvg_synth_value(uint64_t seed, uint64_t idx);
+int    mvg_synth_fill_host(double* dst, int64_t ld, int64_t m, int64_t k,
+                           int64_t row_off, int64_t col_off, int64_t n_cols_global, uint64_t seed);
+int    mvg_synth_fill_device(double* d_dst, int64_t ld, int64_t m, int64_t k,
+                             int64_t row_off, int64_t col_off, int64_t n_cols_global,
+                             uint64_t seed, void* stream);
+
+/* ------------------------------------------------------------------ device helpers */
+int mvg_device_count(int* n);
+int mvg_set_device(int dev);
+int mvg_malloc(void** dptr, size_t bytes);
+int mvg_free(void* dptr);
+int mvg_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int mvg_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int mvg_stream_sync(void* stream);
+int mvg_host_register(void* ptr, size_t bytes);     /* pin caller-owned host memory */
+int mvg_host_unregister(void* ptr);
+
+/* ------------------------------------------------------------------ the hot kernel
+ * y[i] = sum_j A[i*lda + j] * x[j], i < m, j < k (fp64, row-major, lda >= k).
+ * Device pointers; asynchronous on `stream`. Results match the reference's sequential
+ * left-to-right sum (src/matr_utils.c:87-93) to <= 1e-12 relative per element for
+ * non-negative data (different, fixed, run-to-run deterministic summation order).
+ * m == 0 or k == 0 is valid (k == 0 writes zeros, as the reference's `sum = 0`). */
+int mvg_gemv(const double* d_A, int64_t lda, const double* d_x, double* d_y,
+             int64_t m, int64_t k, void* stream);
+
+/* Same, with an explicit kernel variant (benchmarks / tests):
+ *   0 = auto, 1 = wave-per-row x4 rows, 2 = 16-lane groups, 3 = scalar (no 16-B loads),
+ *   4 = wave-per-row x2 rows, 5 = wave-per-row x8 rows, 6 = 8-lane groups ... */
+int mvg_gemv_variant(const double* d_A, int64_t lda, const double* d_x, double* d_y,
+                     int64_t m, int64_t k, int variant, void* stream);
+int mvg_gemv_variant_count(void);
+const char* mvg_gemv_variant_name(int variant);
+
+/* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */
+int mvg_stream_read(const double* d_src, int64_t n, double* d_sink, void* stream);
+
+/* ------------------------------------------------------------------ communicators (RCCL)
+ * One communicator object per process covers all devices this process drives:
+ *   mvg_comm_init_all : single process, G devices (the executables' model; ncclCommInitAll)
+ *   mvg_comm_init_rank: one process per device (torch.distributed.run model); the caller
+ *                       moves the 128-byte unique id from rank 0 to every rank. */
+typedef struct mvg_comm mvg_comm;
+#define MVG_UNIQUE_ID_BYTES 128
+int mvg_comm_unique_id(unsigned char out[MVG_UNIQUE_ID_BYTES]);
+int mvg_comm_init_all(mvg_comm** out, int ndev, const int* devlist);
+int mvg_comm_init_rank(mvg_comm** out, const unsigned char id[MVG_UNIQUE_ID_BYTES],
+                       int nranks, int rank, int device);
+int mvg_comm_size(const mvg_comm* c, int* nranks);
+int mvg_comm_local_count(const mvg_comm* c, int* nlocal);
+int mvg_comm_local_rank(const mvg_comm* c, int local_index, int* rank, int* device);
+int mvg_comm_destroy(mvg_comm* c);
+
+/* ------------------------------------------------------------------ engine
+ * The distributed multiplier: one object per (alg, R, C, comm). Holds, per local device,
+ * the shard of A, the x segment, the partial y and (on rank 0) the full y.
+ *   distribute : host A/x on the root (rank 0's process) -> device shards (H2D, the
+ *                Scatter/Bcast/Pack+Send of the reference). A_host == NULL on non-root.
+ *   fill_synth : device-resident inputs, generated on each device (no host copy).
+ *   multiply   : local GEMV on every device + the exchange step
+ *                (row: ncclGather of y; col: ncclReduce(SUM); block: ncclReduce(SUM) on each
+ *                 grid-row communicator, then ncclGather of the row leaders' slices).
+ *                Asynchronous on the engine's streams; mvg_engine_sync waits.
+ *   collect    : y (R doubles) -> host on the root.  */
+typedef struct mvg_engine mvg_engine;
+int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm* comm);
+int mvg_engine_shard(const mvg_engine* e, int local_index, mvg_shard* out);
+int mvg_engine_distribute(mvg_engine* e, const double* A_host, const double* x_host);
+int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x);
+int mvg_engine_multiply(mvg_engine* e);
+int mvg_engine_sync(mvg_engine* e);
+int mvg_engine_collect(mvg_engine* e, double* y_host);
+/* per-local-device stream (hipStream_t as void*), e.g. for hipEvent timing by the caller */
+int mvg_engine_stream(const mvg_engine* e, int local_index, void** stream);
+/* Average GEMV kernel time (ms) over the multiply calls since the last reset, measured with
+ * hipEvents bracketing the kernel on each local device's stream (max over local devices). */
+int mvg_engine_kernel_timing(mvg_engine* e, int enable);
+int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches);
+int mvg_engine_destroy(mvg_engine* e);
+
+/* ------------------------------------------------------------------ text I/O (src/matr_utils.c)
+ * Same file names under the same directory convention: <dir>/matrix_<R>_<C>.txt,
+ * <dir>/vector_<n>.txt (dir "./data" in the executables, matr_utils.c:45,68). Whitespace
+ * separated "%lf" tokens, row-major. Parsing is strtod (== fscanf "%lf") on an mmap'd file,
+ * split over threads; 64-bit indexing. Returns MVG_E_IO if the file is missing or short. */
+int mvg_matrix_filename(int64_t R, int64_t C, char* buf, size_t buflen);
+int mvg_vector_filename(int64_t n, char* buf, size_t buflen);
+int mvg_load_matr(const char* dir, int64_t R, int64_t C, double* A);
+int mvg_load_vec(const char* dir, int64_t n, double* x);
+int mvg_write_vec(const char* path, const double* v, int64_t n);   /* "%.17g\n" per value */
+int mvg_write_matr_synth(const char* path, int64_t R, int64_t C, uint64_t seed); /* "%.4f " */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MATVEC_GPU_H */

@@ -1,0 +1,138 @@
+"""ctypes binding of libmatvec_gpu.so (the C-ABI declared in include/matvec_gpu.h).
+
+The library is the product: there is no Python or CPU fallback for any compute call. If the
+shared object is missing this module raises at import time with the build command to run.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmatvec_gpu.so")
+
+MVG_OK = 0
+MVG_E_INVALID = -1
+MVG_E_INDIVISIBLE = -2
+MVG_E_HIP = -3
+MVG_E_RCCL = -4
+MVG_E_IO = -5
+MVG_E_NOMEM = -6
+MVG_E_STATE = -7
+
+ALG_ROWWISE, ALG_COLWISE, ALG_BLOCKWISE = 0, 1, 2
+ALG_NAMES = {ALG_ROWWISE: "rowwise", ALG_COLWISE: "colwise", ALG_BLOCKWISE: "blockwise"}
+ALG_BY_NAME = {v: k for k, v in ALG_NAMES.items()}
+
+SEED_A = 42
+SEED_X = 4242
+UNIQUE_ID_BYTES = 128
+
+
+class MvgError(RuntimeError):
+    def __init__(self, code: int, where: str, detail: str):
+        self.code = code
+        super().__init__(f"{where} failed ({code}): {detail}")
+
+
+class IndivisibleError(MvgError):
+    """Shape does not split over the rank count (the reference's "ERROR!!!" case)."""
+
+
+class Shard(C.Structure):
+    """mvg_shard: the slice of the global problem one rank owns."""
+
+    _fields_ = [
+        ("alg", C.c_int), ("nranks", C.c_int), ("rank", C.c_int),
+        ("grid_rows", C.c_int), ("grid_cols", C.c_int), ("grid_r", C.c_int), ("grid_c", C.c_int),
+        ("R", C.c_int64), ("C", C.c_int64),
+        ("row_off", C.c_int64), ("col_off", C.c_int64), ("n_rows", C.c_int64), ("n_cols", C.c_int64),
+        ("y_off", C.c_int64), ("y_len", C.c_int64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_p = C.c_void_p
+_i64 = C.c_int64
+_dp = C.POINTER(C.c_double)
+
+# name -> (restype, argtypes); the order follows include/matvec_gpu.h
+SIGNATURES = {
+    "mvg_version": (C.c_char_p, []),
+    "mvg_strerror": (C.c_char_p, [C.c_int]),
+    "mvg_last_error": (C.c_char_p, []),
+    "mvg_grid_shape": (C.c_int, [_i64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "mvg_plan_shard": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.POINTER(Shard)]),
+    "mvg_synth_value": (C.c_double, [C.c_uint64, C.c_uint64]),
+    "mvg_synth_fill_host": (C.c_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, C.c_uint64]),
+    "mvg_synth_fill_device": (C.c_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, C.c_uint64, _p]),
+    "mvg_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "mvg_set_device": (C.c_int, [C.c_int]),
+    "mvg_malloc": (C.c_int, [C.POINTER(_p), C.c_size_t]),
+    "mvg_free": (C.c_int, [_p]),
+    "mvg_memcpy_h2d": (C.c_int, [_p, _p, C.c_size_t, _p]),
+    "mvg_memcpy_d2h": (C.c_int, [_p, _p, C.c_size_t, _p]),
+    "mvg_stream_sync": (C.c_int, [_p]),
+    "mvg_host_register": (C.c_int, [_p, C.c_size_t]),
+    "mvg_host_unregister": (C.c_int, [_p]),
+    "mvg_gemv": (C.c_int, [_p, _i64, _p, _p, _i64, _i64, _p]),
+    "mvg_gemv_variant": (C.c_int, [_p, _i64, _p, _p, _i64, _i64, C.c_int, _p]),
+    "mvg_gemv_variant_count": (C.c_int, []),
+    "mvg_gemv_variant_name": (C.c_char_p, [C.c_int]),
+    "mvg_stream_read": (C.c_int, [_p, _i64, _p, _p]),
+    "mvg_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "mvg_comm_init_all": (C.c_int, [C.POINTER(_p), C.c_int, C.POINTER(C.c_int)]),
+    "mvg_comm_init_rank": (C.c_int, [C.POINTER(_p), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "mvg_comm_size": (C.c_int, [_p, C.POINTER(C.c_int)]),
+    "mvg_comm_local_count": (C.c_int, [_p, C.POINTER(C.c_int)]),
+    "mvg_comm_local_rank": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "mvg_comm_destroy": (C.c_int, [_p]),
+    "mvg_engine_create": (C.c_int, [C.POINTER(_p), C.c_int, _i64, _i64, _p]),
+    "mvg_engine_shard": (C.c_int, [_p, C.c_int, C.POINTER(Shard)]),
+    "mvg_engine_distribute": (C.c_int, [_p, _p, _p]),
+    "mvg_engine_fill_synth": (C.c_int, [_p, C.c_uint64, C.c_uint64]),
+    "mvg_engine_multiply": (C.c_int, [_p]),
+    "mvg_engine_sync": (C.c_int, [_p]),
+    "mvg_engine_collect": (C.c_int, [_p, _p]),
+    "mvg_engine_stream": (C.c_int, [_p, C.c_int, C.POINTER(_p)]),
+    "mvg_engine_kernel_timing": (C.c_int, [_p, C.c_int]),
+    "mvg_engine_kernel_ms": (C.c_int, [_p, C.POINTER(C.c_double), C.POINTER(_i64)]),
+    "mvg_engine_destroy": (C.c_int, [_p]),
+    "mvg_matrix_filename": (C.c_int, [_i64, _i64, C.c_char_p, C.c_size_t]),
+    "mvg_vector_filename": (C.c_int, [_i64, C.c_char_p, C.c_size_t]),
+    "mvg_load_matr": (C.c_int, [C.c_char_p, _i64, _i64, _p]),
+    "mvg_load_vec": (C.c_int, [C.c_char_p, _i64, _p]),
+    "mvg_write_vec": (C.c_int, [C.c_char_p, _p, _i64]),
+    "mvg_write_matr_synth": (C.c_int, [C.c_char_p, _i64, _i64, C.c_uint64]),
+}
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: the HIP library is required (no CPU fallback). "
+            "Build it with `make -C <repo>` or `python -c 'import __graft_entry__ as g; g.build()'`."
+        )
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, where: str) -> None:
+    if rc != MVG_OK:
+        detail = lib.mvg_last_error().decode(errors="replace")
+        cls = IndivisibleError if rc == MVG_E_INDIVISIBLE else MvgError
+        raise cls(rc, where, detail)
+
+
+def ptr(a) -> int:
+    """Address of a numpy array's data (host) as an int for ctypes."""
+    return a.ctypes.data

@@ -1,0 +1,72 @@
+// Internal helpers shared by the libmatvec_gpu translation units (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/matvec_gpu.h"
+
+namespace mvg {
+
+// Last error text for mvg_last_error(); thread-local like errno.
+void set_error(const std::string& msg);
+const std::string& get_error();
+
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define MVG_HIP(call)                                                     \
+    do {                                                                  \
+        hipError_t _e = (call);                                           \
+        if (_e != hipSuccess) return ::mvg::hip_fail(_e, #call);          \
+    } while (0)
+
+// ----- synthetic generator (spec in include/matvec_gpu.h) ---------------------------
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ULL;
+
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) { return mix64(x + kGamma); }
+
+__host__ __device__ inline uint64_t mulhi_10000(uint64_t z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(z, 10000ULL);
+#else
+    return (uint64_t)(((unsigned __int128)z * 10000u) >> 64);
+#endif
+}
+
+// s0 = splitmix64(seed); value = floor(splitmix64(s0 + idx*gamma) * 1e4 / 2^64) / 1e4
+__host__ __device__ inline double synth_value(uint64_t s0, uint64_t idx) {
+    const uint64_t z = splitmix64(s0 + idx * kGamma);
+    return (double)mulhi_10000(z) / 10000.0;
+}
+
+// Static split of [0, n) over the host's threads (capped by MVG_THREADS / 64).
+// `serial` forces one thread (small jobs).
+template <class F>
+void parallel_for(int64_t n, F&& body, bool serial = false) {
+    int nt = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("MVG_THREADS")) nt = atoi(e);
+    if (nt < 1) nt = 1;
+    if (nt > 64) nt = 64;
+    if (nt > n) nt = (int)(n > 0 ? n : 1);
+    if (serial || nt == 1) {
+        body((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t b = n * t / nt, e = n * (t + 1) / nt;
+        th.emplace_back([&body, b, e] { body(b, e); });
+    }
+    for (auto& t : th) t.join();
+}
+
+}  // namespace mvg

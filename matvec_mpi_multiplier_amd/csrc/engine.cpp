@@ -1,0 +1,569 @@
+// Communicators (RCCL over xGMI) and the distributed multiplier engine.
+//
+// The engine is the MI355X replacement for what the three reference drivers do around the
+// local product, one algorithm per object:
+//
+//   ROWWISE   distribute: MPI_Scatter(rows) + MPI_Bcast(x)          rowwise.c:12-51
+//             exchange  : MPI_Gather(y pieces, rank order)          rowwise.c:141
+//             here      : H2D row shard (or root->peer ncclSend), ncclGather of y to rank 0
+//   COLWISE   distribute: MPI_Type_vector + MPI_Pack + MPI_Send strips, MPI_Scatter(x)
+//                                                                   colwise.c:11-102
+//             exchange  : MPI_Reduce(SUM) of partial y              colwise.c:124
+//             here      : 2-D H2D into a packed strip, ncclReduce(fp64, sum) to rank 0
+//   BLOCKWISE distribute: block Pack + Send, x segment Send         blockwise.c:17-141
+//             exchange  : root Recv(ANY_SOURCE) + y[(src/c)*lr+j] += partial
+//                                                                   blockwise.c:144-210
+//             here      : ncclReduce(sum) over each grid-row communicator to the row leader
+//                         (grid column 0), then ncclGather of the r leader slices to rank 0.
+//                         Fixed order: deterministic, unlike the reference's arrival order.
+//
+// One process may drive several devices (mvg_comm_init_all: the executables) or exactly one
+// (mvg_comm_init_rank: one process per GPU under torch.distributed.run). Every collective
+// is issued for all local devices inside ncclGroupStart/End, so both models share one path.
+#include <rccl/rccl.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+using namespace mvg;
+
+namespace {
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    set_error(std::string(what) + ": " + ncclGetErrorString(r));
+    return MVG_E_RCCL;
+}
+
+#define MVG_NCCL(call)                                                  \
+    do {                                                                \
+        ncclResult_t _r = (call);                                       \
+        if (_r != ncclSuccess) return nccl_fail(_r, #call);             \
+    } while (0)
+
+struct LocalRank {
+    int rank = 0;
+    int device = 0;
+    ncclComm_t comm = nullptr;
+};
+
+}  // namespace
+
+struct mvg_comm {
+    int nranks = 0;
+    std::vector<LocalRank> locals;
+};
+
+namespace {
+
+struct Shard {
+    mvg_shard plan{};
+    int device = 0;
+    int rank = 0;
+    ncclComm_t world = nullptr;
+    ncclComm_t row_comm = nullptr;  // block-split: the c ranks of this grid row
+    ncclComm_t col_comm = nullptr;  // block-split: the r row leaders (grid column 0)
+    hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;
+    double* dA = nullptr;
+    double* dx = nullptr;
+    double* dy_part = nullptr;  // local product: y_len (row/block) or R (col) doubles
+    double* dy_row = nullptr;   // block-split row leader: reduced slice (lr doubles)
+    double* dy = nullptr;       // rank 0: the full y (R doubles)
+    double* stage[2] = {nullptr, nullptr};  // root: staging for root->peer sends (rank mode)
+    size_t stage_elems = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    size_t ev_used = 0;
+};
+
+}  // namespace
+
+struct mvg_engine {
+    int alg = 0;
+    int64_t R = 0, C = 0;
+    int nranks = 0;
+    bool single_process = false;  // all ranks in this process
+    bool always_collect = false;  // run the collectives even at nranks == 1 (tests)
+    bool distributed = false;
+    bool timing = false;
+    double kernel_ms_sum = 0.0;
+    int64_t kernel_launches = 0;
+    std::vector<Shard> shards;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = 0;
+    DeviceGuard() { (void)hipGetDevice(&prev); }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+int alloc_doubles(double** p, int64_t n) {
+    if (n <= 0) {
+        *p = nullptr;
+        return MVG_OK;
+    }
+    hipError_t e = hipMalloc((void**)p, (size_t)n * sizeof(double));
+    if (e != hipSuccess) {
+        hip_fail(e, "hipMalloc");
+        return MVG_E_NOMEM;
+    }
+    return MVG_OK;
+}
+
+void free_shard(Shard& s) {
+    (void)hipSetDevice(s.device);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.copy_stream) (void)hipStreamSynchronize(s.copy_stream);
+    for (double* p : {s.dA, s.dx, s.dy_part, s.dy_row, s.dy, s.stage[0], s.stage[1]})
+        if (p) (void)hipFree(p);
+    for (auto& ev : s.ev_pool) {
+        (void)hipEventDestroy(ev.first);
+        (void)hipEventDestroy(ev.second);
+    }
+    s.ev_pool.clear();
+    if (s.row_comm) (void)ncclCommDestroy(s.row_comm);
+    if (s.col_comm) (void)ncclCommDestroy(s.col_comm);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.copy_stream) (void)hipStreamDestroy(s.copy_stream);
+    s = Shard{};
+}
+
+// 2-D host -> device copy of a shard region into a packed device buffer (pitch = cols).
+int h2d_region(double* dst, const double* host, int64_t ld_host, int64_t rows, int64_t cols,
+               hipStream_t s) {
+    if (rows == 0 || cols == 0) return MVG_OK;
+    if (cols == ld_host) {
+        MVG_HIP(hipMemcpyAsync(dst, host, (size_t)(rows * cols) * sizeof(double),
+                               hipMemcpyHostToDevice, s));
+    } else {
+        MVG_HIP(hipMemcpy2DAsync(dst, (size_t)cols * sizeof(double), host,
+                                 (size_t)ld_host * sizeof(double), (size_t)cols * sizeof(double),
+                                 (size_t)rows, hipMemcpyHostToDevice, s));
+    }
+    return MVG_OK;
+}
+
+// x segment that a shard needs: full x (row), strip segment (col), block column segment.
+inline int64_t x_off(const mvg_shard& p) { return p.col_off; }
+inline int64_t x_len(const mvg_shard& p) { return p.n_cols; }
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------ communicators
+int mvg_comm_unique_id(unsigned char out[MVG_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == MVG_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    if (!out) return fail(MVG_E_INVALID, "null");
+    ncclUniqueId id;
+    MVG_NCCL(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof id);
+    return MVG_OK;
+}
+
+int mvg_comm_init_all(mvg_comm** out, int ndev, const int* devlist) {
+    if (!out || ndev <= 0) return fail(MVG_E_INVALID, "mvg_comm_init_all: bad arguments");
+    *out = nullptr;
+    std::vector<int> devs(ndev);
+    for (int i = 0; i < ndev; ++i) devs[i] = devlist ? devlist[i] : i;
+    std::vector<ncclComm_t> comms(ndev);
+    DeviceGuard g;
+    MVG_NCCL(ncclCommInitAll(comms.data(), ndev, devs.data()));
+    mvg_comm* c = new mvg_comm;
+    c->nranks = ndev;
+    for (int i = 0; i < ndev; ++i) c->locals.push_back(LocalRank{i, devs[i], comms[i]});
+    *out = c;
+    return MVG_OK;
+}
+
+int mvg_comm_init_rank(mvg_comm** out, const unsigned char id[MVG_UNIQUE_ID_BYTES], int nranks,
+                       int rank, int device) {
+    if (!out || !id || nranks <= 0 || rank < 0 || rank >= nranks)
+        return fail(MVG_E_INVALID, "mvg_comm_init_rank: bad arguments");
+    *out = nullptr;
+    MVG_HIP(hipSetDevice(device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    ncclComm_t comm;
+    MVG_NCCL(ncclCommInitRank(&comm, nranks, uid, rank));
+    mvg_comm* c = new mvg_comm;
+    c->nranks = nranks;
+    c->locals.push_back(LocalRank{rank, device, comm});
+    *out = c;
+    return MVG_OK;
+}
+
+int mvg_comm_size(const mvg_comm* c, int* n) {
+    if (!c || !n) return fail(MVG_E_INVALID, "null");
+    *n = c->nranks;
+    return MVG_OK;
+}
+int mvg_comm_local_count(const mvg_comm* c, int* n) {
+    if (!c || !n) return fail(MVG_E_INVALID, "null");
+    *n = (int)c->locals.size();
+    return MVG_OK;
+}
+int mvg_comm_local_rank(const mvg_comm* c, int i, int* rank, int* device) {
+    if (!c || i < 0 || i >= (int)c->locals.size()) return fail(MVG_E_INVALID, "bad local index");
+    if (rank) *rank = c->locals[i].rank;
+    if (device) *device = c->locals[i].device;
+    return MVG_OK;
+}
+int mvg_comm_destroy(mvg_comm* c) {
+    if (!c) return MVG_OK;
+    DeviceGuard g;
+    for (auto& l : c->locals) {
+        (void)hipSetDevice(l.device);
+        if (l.comm) (void)ncclCommDestroy(l.comm);
+    }
+    delete c;
+    return MVG_OK;
+}
+
+// ------------------------------------------------------------------ engine
+int mvg_engine_destroy(mvg_engine* e) {
+    if (!e) return MVG_OK;
+    DeviceGuard g;
+    for (auto& s : e->shards) free_shard(s);
+    delete e;
+    return MVG_OK;
+}
+
+int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm* comm) {
+    if (!out || !comm || R < 0 || C < 0) return fail(MVG_E_INVALID, "mvg_engine_create: bad arguments");
+    *out = nullptr;
+    // Validate the whole grid first (the reference's root-only divisibility check).
+    mvg_shard probe;
+    int rc = mvg_plan_shard(alg, R, C, comm->nranks, 0, &probe);
+    if (rc != MVG_OK) return rc;
+
+    DeviceGuard g;
+    mvg_engine* e = new mvg_engine;
+    e->alg = alg;
+    e->R = R;
+    e->C = C;
+    e->nranks = comm->nranks;
+    e->single_process = (int)comm->locals.size() == comm->nranks;
+    const char* ac = getenv("MVG_ALWAYS_COLLECT");
+    e->always_collect = ac && ac[0] == '1';
+    e->shards.resize(comm->locals.size());
+    auto bail = [&](int code) {
+        mvg_engine_destroy(e);
+        return code;
+    };
+    for (size_t i = 0; i < comm->locals.size(); ++i) {
+        Shard& s = e->shards[i];
+        const LocalRank& l = comm->locals[i];
+        s.device = l.device;
+        s.rank = l.rank;
+        s.world = l.comm;
+        if ((rc = mvg_plan_shard(alg, R, C, comm->nranks, l.rank, &s.plan)) != MVG_OK) return bail(rc);
+        if (hipSetDevice(s.device) != hipSuccess) return bail(fail(MVG_E_HIP, "hipSetDevice"));
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(MVG_E_HIP, "hipStreamCreate"));
+        const mvg_shard& p = s.plan;
+        if ((rc = alloc_doubles(&s.dA, p.n_rows * p.n_cols)) != MVG_OK) return bail(rc);
+        if ((rc = alloc_doubles(&s.dx, x_len(p))) != MVG_OK) return bail(rc);
+        const int64_t part = alg == MVG_ALG_COLWISE ? R : p.y_len;
+        if ((rc = alloc_doubles(&s.dy_part, part)) != MVG_OK) return bail(rc);
+        if (alg == MVG_ALG_BLOCKWISE && p.grid_c == 0 && p.grid_rows > 1)
+            if ((rc = alloc_doubles(&s.dy_row, p.y_len)) != MVG_OK) return bail(rc);
+        if (l.rank == 0)
+            if ((rc = alloc_doubles(&s.dy, R)) != MVG_OK) return bail(rc);
+    }
+    // Block-split sub-communicators: ncclCommSplit is collective over the world, so every
+    // local rank calls it inside one group.
+    if (alg == MVG_ALG_BLOCKWISE && comm->nranks > 1) {
+        ncclResult_t r = ncclGroupStart();
+        for (auto& s : e->shards) {
+            if (r != ncclSuccess) break;
+            (void)hipSetDevice(s.device);
+            r = ncclCommSplit(s.world, s.plan.grid_r, s.plan.grid_c, &s.row_comm, nullptr);
+        }
+        ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit(row)"));
+        if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit(row) group"));
+        r = ncclGroupStart();
+        for (auto& s : e->shards) {
+            if (r != ncclSuccess) break;
+            (void)hipSetDevice(s.device);
+            const int color = s.plan.grid_c == 0 ? 0 : NCCL_SPLIT_NOCOLOR;
+            r = ncclCommSplit(s.world, color, s.plan.grid_r, &s.col_comm, nullptr);
+        }
+        r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit(col)"));
+        if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit(col) group"));
+    }
+    *out = e;
+    return MVG_OK;
+}
+
+int mvg_engine_shard(const mvg_engine* e, int i, mvg_shard* out) {
+    if (!e || !out || i < 0 || i >= (int)e->shards.size()) return fail(MVG_E_INVALID, "bad index");
+    *out = e->shards[i].plan;
+    return MVG_OK;
+}
+
+int mvg_engine_stream(const mvg_engine* e, int i, void** stream) {
+    if (!e || !stream || i < 0 || i >= (int)e->shards.size()) return fail(MVG_E_INVALID, "bad index");
+    *stream = (void*)e->shards[i].stream;
+    return MVG_OK;
+}
+
+int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    DeviceGuard g;
+    int rc;
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        const mvg_shard& p = s.plan;
+        if ((rc = mvg_synth_fill_device(s.dA, p.n_cols, p.n_rows, p.n_cols, p.row_off, p.col_off,
+                                        e->C, seed_a, s.stream)) != MVG_OK)
+            return rc;
+        if ((rc = mvg_synth_fill_device(s.dx, x_len(p), 1, x_len(p), 0, x_off(p), e->C, seed_x,
+                                        s.stream)) != MVG_OK)
+            return rc;
+    }
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        MVG_HIP(hipStreamSynchronize(s.stream));
+    }
+    e->distributed = true;
+    return MVG_OK;
+}
+
+// Root (rank 0's process) holds A and x in host memory, as in every reference driver.
+// Single-process: each device pulls its own shard over its own PCIe link, concurrently.
+// One process per GPU: rank 0 stages each peer's shard through two device buffers and
+// ncclSend's it over xGMI (the reference's sequential root Send loop, colwise.c:33-57),
+// overlapping the next chunk's H2D with the current chunk's send.
+int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    DeviceGuard g;
+    const int64_t C = e->C;
+    Shard* root = nullptr;
+    for (auto& s : e->shards)
+        if (s.rank == 0) root = &s;
+    if (root && (!x || (!A && e->R * C > 0))) return fail(MVG_E_INVALID, "root needs A and x");
+
+    if (e->single_process) {
+        for (auto& s : e->shards) {
+            MVG_HIP(hipSetDevice(s.device));
+            const mvg_shard& p = s.plan;
+            int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
+            if (rc != MVG_OK) return rc;
+            rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
+            if (rc != MVG_OK) return rc;
+        }
+    } else {
+        // exactly one local shard
+        Shard& s = e->shards[0];
+        MVG_HIP(hipSetDevice(s.device));
+        if (s.rank == 0) {
+            const int64_t chunk_bytes = 256ll << 20;
+            if (!s.stage[0]) {
+                s.stage_elems = (size_t)(chunk_bytes / (int64_t)sizeof(double));
+                int rc;
+                if ((rc = alloc_doubles(&s.stage[0], (int64_t)s.stage_elems)) != MVG_OK) return rc;
+                if ((rc = alloc_doubles(&s.stage[1], (int64_t)s.stage_elems)) != MVG_OK) return rc;
+            }
+            hipEvent_t copied[2], sent[2];
+            for (int b = 0; b < 2; ++b) {
+                MVG_HIP(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
+                MVG_HIP(hipEventCreateWithFlags(&sent[b], hipEventDisableTiming));
+                MVG_HIP(hipEventRecord(sent[b], s.stream));
+            }
+            int buf = 0;
+            for (int peer = 1; peer < e->nranks; ++peer) {
+                mvg_shard p;
+                int rc = mvg_plan_shard(e->alg, e->R, C, e->nranks, peer, &p);
+                if (rc != MVG_OK) return rc;
+                // x segment first, then A rows in chunks
+                struct Piece { const double* src; int64_t ld, rows, cols; };
+                std::vector<Piece> pieces;
+                pieces.push_back({x + x_off(p), x_len(p), 1, x_len(p)});
+                const int64_t rows_per = p.n_cols > 0
+                    ? std::max<int64_t>(1, (int64_t)s.stage_elems / p.n_cols) : p.n_rows;
+                for (int64_t r0 = 0; r0 < p.n_rows; r0 += rows_per)
+                    pieces.push_back({A + (p.row_off + r0) * C + p.col_off, C,
+                                      std::min(rows_per, p.n_rows - r0), p.n_cols});
+                for (const Piece& pc : pieces) {
+                    const int64_t n = pc.rows * pc.cols;
+                    if (n == 0) continue;
+                    if (n > (int64_t)s.stage_elems) return fail(MVG_E_INVALID, "row larger than staging");
+                    MVG_HIP(hipStreamWaitEvent(s.copy_stream, sent[buf], 0));
+                    if ((rc = h2d_region(s.stage[buf], pc.src, pc.ld, pc.rows, pc.cols, s.copy_stream)) != MVG_OK)
+                        return rc;
+                    MVG_HIP(hipEventRecord(copied[buf], s.copy_stream));
+                    MVG_HIP(hipStreamWaitEvent(s.stream, copied[buf], 0));
+                    MVG_NCCL(ncclSend(s.stage[buf], (size_t)n, ncclFloat64, peer, s.world, s.stream));
+                    MVG_HIP(hipEventRecord(sent[buf], s.stream));
+                    buf ^= 1;
+                }
+            }
+            // own shard last (MPI_Pack of the root's own strip comes last too, colwise.c:61-69)
+            const mvg_shard& p = s.plan;
+            int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.copy_stream);
+            if (rc != MVG_OK) return rc;
+            if ((rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.copy_stream)) != MVG_OK) return rc;
+            MVG_HIP(hipEventRecord(copied[0], s.copy_stream));
+            MVG_HIP(hipStreamWaitEvent(s.stream, copied[0], 0));
+            for (int b = 0; b < 2; ++b) {
+                (void)hipEventDestroy(copied[b]);
+                (void)hipEventDestroy(sent[b]);
+            }
+        } else {
+            const mvg_shard& p = s.plan;
+            if (x_len(p) > 0)
+                MVG_NCCL(ncclRecv(s.dx, (size_t)x_len(p), ncclFloat64, 0, s.world, s.stream));
+            const int64_t rows_per = p.n_cols > 0
+                ? std::max<int64_t>(1, (int64_t)((256ll << 20) / (int64_t)sizeof(double)) / p.n_cols)
+                : p.n_rows;
+            for (int64_t r0 = 0; r0 < p.n_rows; r0 += rows_per) {
+                const int64_t n = std::min(rows_per, p.n_rows - r0) * p.n_cols;
+                if (n == 0) continue;
+                MVG_NCCL(ncclRecv(s.dA + r0 * p.n_cols, (size_t)n, ncclFloat64, 0, s.world, s.stream));
+            }
+        }
+    }
+    e->distributed = true;
+    return MVG_OK;
+}
+
+int mvg_engine_kernel_timing(mvg_engine* e, int enable) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    int rc = mvg_engine_sync(e);
+    if (rc != MVG_OK) return rc;
+    e->timing = enable != 0;
+    e->kernel_ms_sum = 0.0;
+    e->kernel_launches = 0;
+    return MVG_OK;
+}
+
+int mvg_engine_multiply(mvg_engine* e) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    if (!e->distributed) return fail(MVG_E_STATE, "mvg_engine_multiply before distribute/fill");
+    DeviceGuard g;
+    const bool solo = e->nranks == 1 && !e->always_collect;
+    // 1) local product on every device
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        const mvg_shard& p = s.plan;
+        double* out = solo ? s.dy : s.dy_part;
+        hipEvent_t t0 = nullptr, t1 = nullptr;
+        if (e->timing) {
+            if (s.ev_used == s.ev_pool.size()) {
+                hipEvent_t a, b;
+                MVG_HIP(hipEventCreate(&a));
+                MVG_HIP(hipEventCreate(&b));
+                s.ev_pool.emplace_back(a, b);
+            }
+            t0 = s.ev_pool[s.ev_used].first;
+            t1 = s.ev_pool[s.ev_used].second;
+            ++s.ev_used;
+            MVG_HIP(hipEventRecord(t0, s.stream));
+        }
+        int rc = mvg_gemv(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream);
+        if (rc != MVG_OK) return rc;
+        if (e->timing) MVG_HIP(hipEventRecord(t1, s.stream));
+    }
+    if (solo) return MVG_OK;
+    // 2) the exchange step
+    if (e->alg == MVG_ALG_ROWWISE) {
+        MVG_NCCL(ncclGroupStart());
+        for (auto& s : e->shards) {
+            (void)hipSetDevice(s.device);
+            MVG_NCCL(ncclGather(s.dy_part, s.dy ? s.dy : s.dy_part, (size_t)s.plan.y_len, ncclFloat64, 0, s.world, s.stream));
+        }
+        MVG_NCCL(ncclGroupEnd());
+    } else if (e->alg == MVG_ALG_COLWISE) {
+        MVG_NCCL(ncclGroupStart());
+        for (auto& s : e->shards) {
+            (void)hipSetDevice(s.device);
+            MVG_NCCL(ncclReduce(s.dy_part, s.dy ? s.dy : s.dy_part, (size_t)e->R, ncclFloat64, ncclSum, 0, s.world, s.stream));
+        }
+        MVG_NCCL(ncclGroupEnd());
+    } else {
+        const bool one_row = e->shards[0].plan.grid_rows == 1;
+        // row reduce to the grid-row leader; with a single grid row the leader is the root
+        // and reduces straight into y.
+        MVG_NCCL(ncclGroupStart());
+        for (auto& s : e->shards) {
+            (void)hipSetDevice(s.device);
+            ncclComm_t rc = s.row_comm ? s.row_comm : s.world;
+            double* dst = one_row ? s.dy : s.dy_row;
+            if (!dst) dst = s.dy_part;  // recvbuff is only used on the root
+            MVG_NCCL(ncclReduce(s.dy_part, dst, (size_t)s.plan.y_len, ncclFloat64, ncclSum, 0, rc, s.stream));
+        }
+        MVG_NCCL(ncclGroupEnd());
+        if (!one_row) {
+            MVG_NCCL(ncclGroupStart());
+            for (auto& s : e->shards) {
+                if (!s.col_comm) continue;
+                (void)hipSetDevice(s.device);
+                MVG_NCCL(ncclGather(s.dy_row, s.dy, (size_t)s.plan.y_len, ncclFloat64, 0, s.col_comm, s.stream));
+            }
+            MVG_NCCL(ncclGroupEnd());
+        }
+    }
+    return MVG_OK;
+}
+
+int mvg_engine_sync(mvg_engine* e) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    DeviceGuard g;
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        MVG_HIP(hipStreamSynchronize(s.copy_stream));
+        MVG_HIP(hipStreamSynchronize(s.stream));
+    }
+    if (e->timing) {
+        // per multiply call: max over local devices, then summed
+        size_t n = e->shards.empty() ? 0 : e->shards[0].ev_used;
+        for (size_t k = 0; k < n; ++k) {
+            float worst = 0.f;
+            for (auto& s : e->shards) {
+                if (k >= s.ev_used) continue;
+                float ms = 0.f;
+                MVG_HIP(hipEventElapsedTime(&ms, s.ev_pool[k].first, s.ev_pool[k].second));
+                worst = std::max(worst, ms);
+            }
+            e->kernel_ms_sum += worst;
+            ++e->kernel_launches;
+        }
+    }
+    for (auto& s : e->shards) s.ev_used = 0;
+    return MVG_OK;
+}
+
+int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches) {
+    if (!e || !avg_ms) return fail(MVG_E_INVALID, "null");
+    int rc = mvg_engine_sync(e);
+    if (rc != MVG_OK) return rc;
+    *avg_ms = e->kernel_launches ? e->kernel_ms_sum / (double)e->kernel_launches : 0.0;
+    if (launches) *launches = e->kernel_launches;
+    return MVG_OK;
+}
+
+int mvg_engine_collect(mvg_engine* e, double* y) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    DeviceGuard g;
+    for (auto& s : e->shards) {
+        if (s.rank != 0) continue;
+        if (!y) return fail(MVG_E_INVALID, "root needs a y buffer");
+        MVG_HIP(hipSetDevice(s.device));
+        if (e->R > 0)
+            MVG_HIP(hipMemcpyAsync(y, s.dy, (size_t)e->R * sizeof(double), hipMemcpyDeviceToHost, s.stream));
+        MVG_HIP(hipStreamSynchronize(s.stream));
+    }
+    return MVG_OK;
+}
+
+}  // extern "C"

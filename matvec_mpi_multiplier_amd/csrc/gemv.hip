@@ -1,0 +1,332 @@
+// fp64 row-major GEMV for gfx950 (MI355X) — the hot kernel of all three multipliers.
+//
+// Replaces multiply_std_rowwise (reference src/matr_utils.c:86-96) and the strip product of
+// multiply_colwise (src/multiplier_colwise.c:105-122, which is the same y = A_s * x_s done as
+// scale-in-place then row-sum). Arithmetic intensity is 2 flop / 8 B, so the roofline is HBM
+// bandwidth; there is nothing for MFMA to do here.
+//
+// Mapping: a wave64 is split into G = 64/LPR lane groups of LPR lanes. Each group owns RPG
+// rows and walks them left to right together, each lane loading 16 B (two fp64, one
+// global_load_dwordx4) per row per sub-step, UNR sub-steps per iteration, so one lane keeps
+// RPG*UNR 16-B loads of A in flight plus UNR loads of x (x is shared by the G*RPG rows of
+// the wave: x traffic is 1/(G*RPG) of A traffic and is served by L1/L2). Per-lane partial
+// sums are FMAs in a fixed order, reduced across the group with xor-shuffles (DPP/permute),
+// so the result is deterministic run to run. LPR = 64 serves long rows (K >= ~1024),
+// LPR = 16/8 serves short rows (the 4,194,304 x 512 tall-skinny config) without idle lanes.
+//
+// A row stride (lda) that is odd, or a misaligned base, cannot use 16-B loads: the scalar
+// variant (8 B per lane, still coalesced) covers it.
+#include "common.h"
+
+#include <mutex>
+
+namespace mvg {
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ dbl2 load2(const double* p) {
+    if constexpr (NT) {
+        return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
+    } else {
+        return *reinterpret_cast<const dbl2*>(p);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ double load1(const double* p) {
+    if constexpr (NT) {
+        return __builtin_nontemporal_load(p);
+    } else {
+        return *p;
+    }
+}
+
+template <int LPR>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+constexpr int kBlock = 256;  // 4 waves
+
+// 16-B path. Requires lda even, A and x 16-B aligned.
+template <int LPR, int RPG, int UNR, bool NT>
+__global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A, int64_t lda,
+                                                   const double* __restrict__ x,
+                                                   double* __restrict__ y, int64_t M,
+                                                   int64_t K) {
+    constexpr int G = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR;
+    const int gl = lane % LPR;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t row0 = (wave * G + g) * RPG;
+
+    const double* arow[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;  // clamp: out-of-range rows re-read a valid row, never stored
+        arow[r] = A + rr * lda;
+    }
+    double acc[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) acc[r] = 0.0;
+
+    constexpr int64_t kStep = 2 * LPR;        // columns one group covers per sub-step
+    constexpr int64_t kChunk = kStep * UNR;   // columns per iteration
+    const int64_t kmain = (K / kChunk) * kChunk;
+    const int64_t c0 = 2 * gl;
+
+    for (int64_t base = c0; base < kmain; base += kChunk) {
+        dbl2 xv[UNR];
+        dbl2 av[RPG][UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) xv[u] = load2<false>(x + base + u * kStep);
+#pragma unroll
+        for (int r = 0; r < RPG; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) av[r][u] = load2<NT>(arow[r] + base + u * kStep);
+#pragma unroll
+        for (int r = 0; r < RPG; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                acc[r] = __builtin_fma(av[r][u].x, xv[u].x, acc[r]);
+                acc[r] = __builtin_fma(av[r][u].y, xv[u].y, acc[r]);
+            }
+    }
+    // column tail: whole pairs, then a possible last odd column
+    for (int64_t c = kmain + c0; c < K; c += kStep) {
+        if (c + 1 < K) {
+            const dbl2 xv = load2<false>(x + c);
+#pragma unroll
+            for (int r = 0; r < RPG; ++r) {
+                const dbl2 a = load2<NT>(arow[r] + c);
+                acc[r] = __builtin_fma(a.x, xv.x, acc[r]);
+                acc[r] = __builtin_fma(a.y, xv.y, acc[r]);
+            }
+        } else {
+            const double xs = x[c];
+#pragma unroll
+            for (int r = 0; r < RPG; ++r) acc[r] = __builtin_fma(arow[r][c], xs, acc[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {
+        const double s = group_sum<LPR>(acc[r]);
+        if (gl == 0 && row0 + r < M) y[row0 + r] = s;
+    }
+}
+
+// 8-B path: any lda, any 8-B alignment.
+template <int LPR, int RPG, int UNR, bool NT>
+__global__ __launch_bounds__(kBlock) void gemv_scalar(const double* __restrict__ A, int64_t lda,
+                                                      const double* __restrict__ x,
+                                                      double* __restrict__ y, int64_t M,
+                                                      int64_t K) {
+    constexpr int G = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR;
+    const int gl = lane % LPR;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t row0 = (wave * G + g) * RPG;
+
+    const double* arow[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    double acc[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) acc[r] = 0.0;
+
+    constexpr int64_t kStep = LPR;
+    constexpr int64_t kChunk = kStep * UNR;
+    const int64_t kmain = (K / kChunk) * kChunk;
+    for (int64_t base = gl; base < kmain; base += kChunk) {
+        double xv[UNR];
+        double av[RPG][UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) xv[u] = x[base + u * kStep];
+#pragma unroll
+        for (int r = 0; r < RPG; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) av[r][u] = load1<NT>(arow[r] + base + u * kStep);
+#pragma unroll
+        for (int r = 0; r < RPG; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) acc[r] = __builtin_fma(av[r][u], xv[u], acc[r]);
+    }
+    for (int64_t c = kmain + gl; c < K; c += kStep) {
+        const double xs = x[c];
+#pragma unroll
+        for (int r = 0; r < RPG; ++r) acc[r] = __builtin_fma(arow[r][c], xs, acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {
+        const double s = group_sum<LPR>(acc[r]);
+        if (gl == 0 && row0 + r < M) y[row0 + r] = s;
+    }
+}
+
+// ------------------------------------------------------------------ variant table
+typedef void (*gemv_fn)(const double*, int64_t, const double*, double*, int64_t, int64_t);
+
+struct Variant {
+    const char* name;
+    gemv_fn fn;
+    int rows_per_wave;  // G * RPG
+    bool vec;           // needs 16-B alignment + even lda
+};
+
+#define VEC(LPR, RPG, UNR, NT) \
+    {"vec_l" #LPR "_r" #RPG "_u" #UNR "_nt" #NT, gemv_vec<LPR, RPG, UNR, NT>, (64 / LPR) * RPG, true}
+#define SCL(LPR, RPG, UNR, NT) \
+    {"scl_l" #LPR "_r" #RPG "_u" #UNR "_nt" #NT, gemv_scalar<LPR, RPG, UNR, NT>, (64 / LPR) * RPG, false}
+
+static const Variant kVariants[] = {
+    {"auto", nullptr, 0, false},   // 0
+    VEC(64, 4, 4, 0),          // 1
+    VEC(64, 4, 4, 1),           // 2
+    VEC(64, 2, 8, 0),          // 3
+    VEC(64, 2, 8, 1),           // 4
+    VEC(64, 8, 2, 1),           // 5
+    VEC(64, 1, 8, 1),           // 6
+    VEC(32, 2, 4, 1),           // 7
+    VEC(16, 2, 4, 1),           // 8
+    VEC(16, 4, 2, 1),           // 9
+    VEC(8, 2, 4, 1),            // 10
+    VEC(16, 1, 8, 1),           // 11
+    SCL(64, 4, 4, 1),           // 12
+    SCL(16, 2, 4, 1),           // 13
+    VEC(64, 4, 8, 1),           // 14
+    VEC(32, 4, 4, 1),           // 15
+};
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+
+// Shape-adaptive choice (see DESIGN.md §4 for the measurements behind it).
+static int pick_variant(int64_t lda, int64_t K, bool aligned) {
+    const bool vec = aligned && (lda % 2 == 0);
+    if (!vec) return K >= 256 ? 12 : 13;
+    if (K >= 2048) return 2;
+    if (K >= 768) return 7;
+    return 8;
+}
+
+static int launch(int v, const double* A, int64_t lda, const double* x, double* y, int64_t M,
+                  int64_t K, hipStream_t s) {
+    const Variant& var = kVariants[v];
+    const int64_t waves = (M + var.rows_per_wave - 1) / var.rows_per_wave;
+    const int64_t blocks = (waves + (kBlock / 64) - 1) / (kBlock / 64);
+    if (blocks > 0x7fffffffLL) return fail(MVG_E_INVALID, "mvg_gemv: too many rows");
+    hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(kBlock), 0, s, A, lda, x, y, M, K);
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
+}
+
+// ------------------------------------------------------------------ other kernels
+__global__ void zero_kernel(double* y, int64_t m) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = 0.0;
+}
+
+__global__ __launch_bounds__(kBlock) void synth_fill_kernel(double* __restrict__ dst, int64_t ld,
+                                                            int64_t m, int64_t k, int64_t row_off,
+                                                            int64_t col_off, int64_t ncols,
+                                                            uint64_t s0) {
+    for (int64_t r = blockIdx.x; r < m; r += gridDim.x) {
+        const uint64_t gbase = (uint64_t)(row_off + r) * (uint64_t)ncols + (uint64_t)col_off;
+        double* d = dst + r * ld;
+        for (int64_t c = threadIdx.x; c < k; c += kBlock) d[c] = synth_value(s0, gbase + c);
+    }
+}
+
+// Read-only stream: HBM ceiling for a pure fp64 read with the same load shape as the GEMV.
+__global__ __launch_bounds__(kBlock) void stream_read_kernel(const double* __restrict__ src,
+                                                             int64_t n2, double* sink) {
+    constexpr int UNR = 8;
+    dbl2 acc = {0.0, 0.0};
+    const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nthr = (int64_t)gridDim.x * kBlock;
+    const dbl2* s = reinterpret_cast<const dbl2*>(src);
+    int64_t i = tid;
+    for (; i + (UNR - 1) * nthr < n2; i += UNR * nthr) {
+        dbl2 v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(s + i + u * nthr);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) acc += v[u];
+    }
+    for (; i < n2; i += nthr) acc += s[i];
+    if (acc.x == -1.0 && acc.y == -2.0) sink[tid] = acc.x;  // never true for real data; keeps loads live
+}
+
+}  // namespace mvg
+
+using namespace mvg;
+
+extern "C" {
+
+int mvg_gemv_variant_count(void) { return kNumVariants; }
+
+const char* mvg_gemv_variant_name(int v) {
+    if (v < 0 || v >= kNumVariants) return "invalid";
+    return kVariants[v].name;
+}
+
+int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m,
+                     int64_t k, int variant, void* stream) {
+    if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv: negative size");
+    if (variant < 0 || variant >= kNumVariants) return fail(MVG_E_INVALID, "mvg_gemv: bad variant");
+    hipStream_t s = (hipStream_t)stream;
+    if (m == 0) return MVG_OK;
+    if (!y) return fail(MVG_E_INVALID, "mvg_gemv: null y");
+    if (k == 0) {
+        hipLaunchKernelGGL(zero_kernel, dim3((unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096)),
+                           dim3(256), 0, s, y, m);
+        MVG_HIP(hipGetLastError());
+        return MVG_OK;
+    }
+    if (!A || !x) return fail(MVG_E_INVALID, "mvg_gemv: null A or x");
+    if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv: lda < k");
+    const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
+    int v = variant == 0 ? pick_variant(lda, k, aligned) : variant;
+    if (kVariants[v].vec && !(aligned && lda % 2 == 0))
+        return fail(MVG_E_INVALID, "mvg_gemv: 16-B variant needs even lda and 16-B aligned A, x");
+    return launch(v, A, lda, x, y, m, k, s);
+}
+
+int mvg_gemv(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
+             void* stream) {
+    return mvg_gemv_variant(A, lda, x, y, m, k, 0, stream);
+}
+
+int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {
+    if (!src || !sink || n < 0 || (n & 1) || ((uintptr_t)src % 16))
+        return fail(MVG_E_INVALID, "mvg_stream_read: need even n, 16-B aligned src, sink");
+    hipLaunchKernelGGL(stream_read_kernel, dim3(256 * 16), dim3(kBlock), 0, (hipStream_t)stream, src,
+                       n / 2, sink);
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
+}
+
+int mvg_synth_fill_device(double* dst, int64_t ld, int64_t m, int64_t k, int64_t row_off,
+                          int64_t col_off, int64_t ncols, uint64_t seed, void* stream) {
+    if (m < 0 || k < 0 || ld < k || row_off < 0 || col_off < 0 || col_off + k > ncols)
+        return fail(MVG_E_INVALID, "mvg_synth_fill_device: bad shape");
+    if (m == 0 || k == 0) return MVG_OK;
+    if (!dst) return fail(MVG_E_INVALID, "mvg_synth_fill_device: null dst");
+    const int64_t blocks = m < 65536 ? m : 65536;
+    hipLaunchKernelGGL(synth_fill_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
+                       (hipStream_t)stream, dst, ld, m, k, row_off, col_off, ncols,
+                       splitmix64(seed));
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
+}
+
+}  // extern "C"

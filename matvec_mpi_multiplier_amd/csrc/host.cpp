@@ -1,0 +1,231 @@
+// Host-side parts of the C-ABI: status/error text, device helpers, the synthetic generator
+// on the host, and the shard planner (pure integer work, no GPU needed).
+#include <math.h>
+#include <string.h>
+
+#include <string>
+
+#include "common.h"
+
+namespace mvg {
+
+static thread_local std::string t_err;
+
+void set_error(const std::string& msg) { t_err = msg; }
+const std::string& get_error() { return t_err; }
+
+int fail(int code, const std::string& msg) {
+    t_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    t_err = std::string(what) + ": " + hipGetErrorString(e);
+    return MVG_E_HIP;
+}
+
+}  // namespace mvg
+
+using namespace mvg;
+
+extern "C" {
+
+const char* mvg_version(void) { return "matvec_gpu 0.1.0 (gfx950)"; }
+
+const char* mvg_strerror(int code) {
+    switch (code) {
+        case MVG_OK: return "ok";
+        case MVG_E_INVALID: return "invalid argument";
+        case MVG_E_INDIVISIBLE: return "shape does not divide over the rank count";
+        case MVG_E_HIP: return "HIP runtime error";
+        case MVG_E_RCCL: return "RCCL error";
+        case MVG_E_IO: return "I/O error";
+        case MVG_E_NOMEM: return "out of memory";
+        case MVG_E_STATE: return "call out of order";
+        default: return "unknown error";
+    }
+}
+
+const char* mvg_last_error(void) { return t_err.c_str(); }
+
+// ------------------------------------------------------------------ planner
+// get_2_most_closest_multipliers (reference src/utils.c:26-37). The reference computes
+// (int)sqrt((double)p) and walks down to the first divisor; same here, with the float
+// sqrt result corrected so a rounding error can never skip the true floor(sqrt(p)).
+int mvg_grid_shape(int64_t p, int* gr, int* gc) {
+    if (p <= 0 || !gr || !gc) return fail(MVG_E_INVALID, "mvg_grid_shape: p must be > 0");
+    int64_t s = (int64_t)sqrt((double)p);
+    while (s * s > p) --s;
+    while ((s + 1) * (s + 1) <= p) ++s;
+    for (int64_t d = s; d > 0; --d) {
+        if (p % d == 0) {
+            *gr = (int)d;
+            *gc = (int)(p / d);
+            return MVG_OK;
+        }
+    }
+    return fail(MVG_E_INVALID, "mvg_grid_shape: unreachable");
+}
+
+// Shard arithmetic of the three drivers:
+//   row-split  : local_n = R / P rows each (rowwise.c:93), rank i owns rows [i*local_n, +local_n)
+//                (MPI_Scatter rank order, rowwise.c:16-37), y slice = its rows (MPI_Gather :141).
+//   col-split  : local_n = C / P columns each (colwise.c:349), rank i owns strip
+//                [i*local_n, +local_n) (Pack offset &matrix[i*local_n], colwise.c:37-38), x segment
+//                i (MPI_Scatter :86-95), partial y over all R rows (MPI_Reduce :124).
+//   block-split: (r, c) = get_2_most_closest_multipliers(P) (blockwise.c:299-302); rank
+//                i*c + j owns block (i, j) of lr x lc (blockwise.c:56,71), x segment j (:79),
+//                partial y slice rows [i*lr, +lr) (blockwise.c:206).
+int mvg_plan_shard(int alg, int64_t R, int64_t C, int P, int rank, mvg_shard* o) {
+    if (!o || R < 0 || C < 0 || P <= 0 || rank < 0 || rank >= P)
+        return fail(MVG_E_INVALID, "mvg_plan_shard: bad arguments");
+    memset(o, 0, sizeof(*o));
+    o->alg = alg;
+    o->nranks = P;
+    o->rank = rank;
+    o->R = R;
+    o->C = C;
+    char msg[256];
+    switch (alg) {
+        case MVG_ALG_ROWWISE: {
+            // rowwise.c:72-75
+            if (R % P != 0) {
+                snprintf(msg, sizeof msg, "%lld mod %d = %lld. Unable to parallellize task.",
+                         (long long)R, P, (long long)(R % P));
+                return fail(MVG_E_INDIVISIBLE, msg);
+            }
+            const int64_t ln = R / P;
+            o->grid_rows = P;
+            o->grid_cols = 1;
+            o->grid_r = rank;
+            o->grid_c = 0;
+            o->row_off = rank * ln;
+            o->n_rows = ln;
+            o->col_off = 0;
+            o->n_cols = C;
+            o->y_off = o->row_off;
+            o->y_len = ln;
+            return MVG_OK;
+        }
+        case MVG_ALG_COLWISE: {
+            // colwise.c:151-154 checks C % P (its message prints R % P by mistake; we print
+            // the quantity that was actually checked).
+            if (C % P != 0) {
+                snprintf(msg, sizeof msg, "%lld mod %d = %lld. Unable to parallellize task.",
+                         (long long)C, P, (long long)(C % P));
+                return fail(MVG_E_INDIVISIBLE, msg);
+            }
+            const int64_t ln = C / P;
+            o->grid_rows = 1;
+            o->grid_cols = P;
+            o->grid_r = 0;
+            o->grid_c = rank;
+            o->row_off = 0;
+            o->n_rows = R;
+            o->col_off = rank * ln;
+            o->n_cols = ln;
+            o->y_off = 0;
+            o->y_len = R;
+            return MVG_OK;
+        }
+        case MVG_ALG_BLOCKWISE: {
+            // blockwise.c:277-281 checks only (R*C) % P ...
+            if (((uint64_t)R * (uint64_t)C) % (uint64_t)P != 0) {
+                snprintf(msg, sizeof msg, "%llu mod %d = %llu. Unable to parallellize task.",
+                         (unsigned long long)((uint64_t)R * (uint64_t)C), P,
+                         (unsigned long long)(((uint64_t)R * (uint64_t)C) % (uint64_t)P));
+                return fail(MVG_E_INDIVISIBLE, msg);
+            }
+            int gr = 1, gc = 1;
+            mvg_grid_shape(P, &gr, &gc);
+            // ... deliberate deviation: the reference then truncates R/r and C/c and silently
+            // drops trailing rows/columns (SURVEY §4 bug 1); we refuse instead.
+            if (R % gr != 0 || C % gc != 0) {
+                snprintf(msg, sizeof msg,
+                         "%lld x %lld does not split over a %d x %d grid. Unable to parallellize task.",
+                         (long long)R, (long long)C, gr, gc);
+                return fail(MVG_E_INDIVISIBLE, msg);
+            }
+            const int64_t lr = R / gr, lc = C / gc;
+            o->grid_rows = gr;
+            o->grid_cols = gc;
+            o->grid_r = rank / gc;
+            o->grid_c = rank % gc;
+            o->row_off = o->grid_r * lr;
+            o->n_rows = lr;
+            o->col_off = o->grid_c * lc;
+            o->n_cols = lc;
+            o->y_off = o->row_off;
+            o->y_len = lr;
+            return MVG_OK;
+        }
+        default:
+            return fail(MVG_E_INVALID, "mvg_plan_shard: unknown algorithm");
+    }
+}
+
+// ------------------------------------------------------------------ synthetic (host)
+double mvg_synth_value(uint64_t seed, uint64_t idx) { return synth_value(splitmix64(seed), idx); }
+
+int mvg_synth_fill_host(double* dst, int64_t ld, int64_t m, int64_t k, int64_t row_off,
+                        int64_t col_off, int64_t ncols, uint64_t seed) {
+    if (m < 0 || k < 0 || ld < k || row_off < 0 || col_off < 0 || col_off + k > ncols)
+        return fail(MVG_E_INVALID, "mvg_synth_fill_host: bad shape");
+    if (m == 0 || k == 0) return MVG_OK;
+    if (!dst) return fail(MVG_E_INVALID, "mvg_synth_fill_host: null dst");
+    const uint64_t s0 = splitmix64(seed);
+    parallel_for(m, [&](int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; ++r) {
+            const uint64_t gbase = (uint64_t)(row_off + r) * (uint64_t)ncols + (uint64_t)col_off;
+            double* d = dst + r * ld;
+            for (int64_t c = 0; c < k; ++c) d[c] = synth_value(s0, gbase + c);
+        }
+    }, m * k < (1 << 20));
+    return MVG_OK;
+}
+
+// ------------------------------------------------------------------ device helpers
+int mvg_device_count(int* n) {
+    if (!n) return fail(MVG_E_INVALID, "null");
+    MVG_HIP(hipGetDeviceCount(n));
+    return MVG_OK;
+}
+int mvg_set_device(int dev) {
+    MVG_HIP(hipSetDevice(dev));
+    return MVG_OK;
+}
+int mvg_malloc(void** p, size_t bytes) {
+    if (!p) return fail(MVG_E_INVALID, "null");
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        hip_fail(e, "hipMalloc");
+        return MVG_E_NOMEM;
+    }
+    return MVG_OK;
+}
+int mvg_free(void* p) {
+    MVG_HIP(hipFree(p));
+    return MVG_OK;
+}
+int mvg_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    MVG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return MVG_OK;
+}
+int mvg_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    MVG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return MVG_OK;
+}
+int mvg_stream_sync(void* stream) {
+    MVG_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return MVG_OK;
+}
+int mvg_host_register(void* ptr, size_t bytes) {
+    MVG_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return MVG_OK;
+}
+int mvg_host_unregister(void* ptr) {
+    MVG_HIP(hipHostUnregister(ptr));
+    return MVG_OK;
+}
+
+}  // extern "C"

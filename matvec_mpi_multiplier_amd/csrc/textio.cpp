@@ -1,0 +1,211 @@
+// Text matrix/vector I/O with the reference's file contract (src/matr_utils.c:9-83):
+//   <dir>/matrix_<R>_<C>.txt   (build_matrix_filename, matr_utils.c:9-12)
+//   <dir>/vector_<n>.txt       (build_vector_filename, matr_utils.c:15-18)
+// whitespace-separated tokens read row-major with "%lf" (matr_utils.c:55-59, 78-80).
+//
+// The reference parses with one fscanf per value; at 16384^2 and up (1.9-120 GB of text)
+// that is impractical, so here the file is mmap'd, split into per-thread ranges on
+// whitespace boundaries, tokens are counted, prefix-summed, then parsed with strtod (the
+// conversion fscanf("%lf") performs), so the doubles are bit-identical to the reference's.
+// Differences, all deliberate: 64-bit indices; a file with fewer tokens than R*C is an error
+// (the reference ignores fscanf's return and leaves garbage); the file is closed.
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+using namespace mvg;
+
+namespace {
+
+inline bool is_space(char c) {
+    return c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
+}
+
+// Parse the first n tokens of the file into out. Returns MVG_OK / MVG_E_IO.
+int parse_file(const std::string& path, int64_t n, double* out) {
+    int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) return fail(MVG_E_IO, "Unable to open '" + path + "': " + strerror(errno));
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return fail(MVG_E_IO, "stat failed for '" + path + "'");
+    }
+    const size_t len = (size_t)st.st_size;
+    if (n == 0) {
+        close(fd);
+        return MVG_OK;
+    }
+    if (len == 0) {
+        close(fd);
+        return fail(MVG_E_IO, "'" + path + "' is empty");
+    }
+    const char* base = (const char*)mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (base == MAP_FAILED) return fail(MVG_E_IO, "mmap failed for '" + path + "'");
+    (void)madvise((void*)base, len, MADV_SEQUENTIAL);
+
+    int nt = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("MVG_THREADS")) nt = atoi(e);
+    if (nt < 1) nt = 1;
+    if (nt > 64) nt = 64;
+    if (len < (1u << 20)) nt = 1;
+    // range t = [cut[t], cut[t+1]); cuts moved forward to the next whitespace so that no
+    // token straddles two ranges.
+    std::vector<size_t> cut(nt + 1);
+    for (int t = 0; t <= nt; ++t) {
+        size_t c = len * (size_t)t / (size_t)nt;
+        if (t > 0 && t < nt)
+            while (c < len && !is_space(base[c])) ++c;
+        cut[t] = c;
+    }
+    for (int t = 1; t <= nt; ++t)
+        if (cut[t] < cut[t - 1]) cut[t] = cut[t - 1];
+
+    std::vector<int64_t> count(nt, 0);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                int64_t k = 0;
+                bool in = false;
+                for (size_t i = cut[t]; i < cut[t + 1]; ++i) {
+                    const bool sp = is_space(base[i]);
+                    if (!sp && !in) ++k;
+                    in = !sp;
+                }
+                count[t] = k;
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<int64_t> start(nt + 1, 0);
+    for (int t = 0; t < nt; ++t) start[t + 1] = start[t] + count[t];
+    if (start[nt] < n) {
+        munmap((void*)base, len);
+        return fail(MVG_E_IO, "'" + path + "' holds " + std::to_string(start[nt]) +
+                                  " values, expected " + std::to_string(n));
+    }
+    std::vector<int> bad(nt, 0);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                int64_t k = start[t];
+                size_t i = cut[t];
+                const size_t end = cut[t + 1];
+                char buf[128];
+                while (i < end && k < n) {
+                    while (i < end && is_space(base[i])) ++i;
+                    if (i >= end) break;
+                    size_t j = i;
+                    while (j < end && !is_space(base[j])) ++j;
+                    const size_t tl = j - i;
+                    if (tl < sizeof(buf)) {
+                        memcpy(buf, base + i, tl);
+                        buf[tl] = '\0';
+                        char* ep = nullptr;
+                        out[k] = strtod(buf, &ep);
+                        if (ep == buf) bad[t] = 1;
+                    } else {
+                        std::string tok(base + i, tl);
+                        char* ep = nullptr;
+                        out[k] = strtod(tok.c_str(), &ep);
+                        if (ep == tok.c_str()) bad[t] = 1;
+                    }
+                    ++k;
+                    i = j;
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    munmap((void*)base, len);
+    for (int t = 0; t < nt; ++t)
+        if (bad[t]) return fail(MVG_E_IO, "'" + path + "' holds a token that is not a number");
+    return MVG_OK;
+}
+
+std::string join(const char* dir, const std::string& name) {
+    std::string d = dir ? dir : ".";
+    if (!d.empty() && d.back() != '/') d += '/';
+    return d + name;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mvg_matrix_filename(int64_t R, int64_t C, char* buf, size_t buflen) {
+    if (!buf) return fail(MVG_E_INVALID, "null");
+    int n = snprintf(buf, buflen, "matrix_%lld_%lld.txt", (long long)R, (long long)C);
+    return (n < 0 || (size_t)n >= buflen) ? fail(MVG_E_INVALID, "buffer too small") : MVG_OK;
+}
+
+int mvg_vector_filename(int64_t n_elems, char* buf, size_t buflen) {
+    if (!buf) return fail(MVG_E_INVALID, "null");
+    int n = snprintf(buf, buflen, "vector_%lld.txt", (long long)n_elems);
+    return (n < 0 || (size_t)n >= buflen) ? fail(MVG_E_INVALID, "buffer too small") : MVG_OK;
+}
+
+int mvg_load_matr(const char* dir, int64_t R, int64_t C, double* A) {
+    if (R < 0 || C < 0 || (!A && R * C > 0)) return fail(MVG_E_INVALID, "mvg_load_matr: bad arguments");
+    char name[128];
+    mvg_matrix_filename(R, C, name, sizeof name);
+    return parse_file(join(dir, name), R * C, A);
+}
+
+int mvg_load_vec(const char* dir, int64_t n, double* x) {
+    if (n < 0 || (!x && n > 0)) return fail(MVG_E_INVALID, "mvg_load_vec: bad arguments");
+    char name[128];
+    mvg_vector_filename(n, name, sizeof name);
+    return parse_file(join(dir, name), n, x);
+}
+
+int mvg_write_vec(const char* path, const double* v, int64_t n) {
+    if (!path || n < 0 || (!v && n > 0)) return fail(MVG_E_INVALID, "mvg_write_vec: bad arguments");
+    FILE* f = fopen(path, "w");
+    if (!f) return fail(MVG_E_IO, std::string("Unable to create '") + path + "'");
+    for (int64_t i = 0; i < n; ++i) fprintf(f, "%.17g\n", v[i]);
+    if (fclose(f) != 0) return fail(MVG_E_IO, std::string("write failed for '") + path + "'");
+    return MVG_OK;
+}
+
+// "%.4f " per value, one matrix row per line (the reference's numpy-written format,
+// README.md:32). Rows are formatted in parallel into per-thread buffers, written in order.
+int mvg_write_matr_synth(const char* path, int64_t R, int64_t C, uint64_t seed) {
+    if (!path || R < 0 || C < 0) return fail(MVG_E_INVALID, "mvg_write_matr_synth: bad arguments");
+    FILE* f = fopen(path, "w");
+    if (!f) return fail(MVG_E_IO, std::string("Unable to create '") + path + "'");
+    const uint64_t s0 = splitmix64(seed);
+    const int64_t rows_per_batch = C > 0 ? std::max<int64_t>(1, (64ll << 20) / (C * 8)) : R;
+    for (int64_t r0 = 0; r0 < R; r0 += rows_per_batch) {
+        const int64_t r1 = std::min(R, r0 + rows_per_batch);
+        std::vector<std::string> lines(r1 - r0);
+        parallel_for(r1 - r0, [&](int64_t a, int64_t b) {
+            char tmp[32];
+            for (int64_t r = a; r < b; ++r) {
+                std::string& s = lines[r];
+                s.reserve((size_t)C * 7 + 1);
+                const uint64_t gbase = (uint64_t)(r0 + r) * (uint64_t)C;
+                for (int64_t c = 0; c < C; ++c) {
+                    int l = snprintf(tmp, sizeof tmp, "%.4f ", synth_value(s0, gbase + c));
+                    s.append(tmp, (size_t)l);
+                }
+                s.push_back('\n');
+            }
+        }, (r1 - r0) * C < (1 << 16));
+        for (auto& s : lines) fwrite(s.data(), 1, s.size(), f);
+    }
+    if (fclose(f) != 0) return fail(MVG_E_IO, std::string("write failed for '") + path + "'");
+    return MVG_OK;
+}
+
+}  // extern "C"
