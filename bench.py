@@ -1,0 +1,253 @@
+"""Benchmark: device-resident distributed fp64 GEMV (BASELINE.json metric) on N MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--alg rowwise|colwise|blockwise]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+Workload (BASELINE.json configs[1], weak-scaled): every GPU owns a 16384 x 16384 fp64 row
+shard of a (16384*N) x 16384 matrix (N = 1: exactly config 2, "Square N=16384 fp64 row-split
+on 1 MI355X"), inputs synthetic (include/matvec_gpu.h spec) and resident in HBM. One step =
+one pass of the hot path: the HIP GEMV on every shard + the RCCL exchange (ncclGather of y
+to rank 0). K steps are timed between barrier + device synchronize on both sides; the time
+is the max over ranks; value = algorithmic bytes of all ranks / that time.
+
+Also reported: `roofline` (the GEMV kernel alone: bytes per launch / its mean duration from
+HIP events on the engine stream; peak 8 TB/s; `traffic` from the committed rocprofv3 PMC
+summary when one matches this configuration), `cpu_baseline` (rank 0 at N = 1: the oracle's
+restatement of the reference's MPI loop timed on this host's cores, reference timing
+semantics), and `end_to_end` (distribution from the root's host memory + multiply + y on
+the root, the reference's timing semantics).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+SHARD = 16384  # rows per GPU and columns (config 2)
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--alg", default="rowwise", choices=["rowwise", "colwise", "blockwise"])
+    ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
+    ap.add_argument("--cols", type=int, default=SHARD)
+    ap.add_argument("--e2e-iters", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(alg: str, R: int, C: int, n: int):
+    """HBM bytes per GEMV launch from the committed rocprofv3 PMC summary for this config
+    (profiles/*pmc*.json written by tools/pmc_traffic.py), or None."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("alg") == alg and d.get("R") == R // n and d.get("C") == C:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+    return None, None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd import multiplier as mm
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = args.gpus
+    if world != n:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    R = args.rows if args.rows is not None else SHARD * n
+    C = args.cols
+    comm = mm.Comm.from_process_group(local) if distributed else mm.Comm.init_all([local])
+    eng = mm.Multiplier(args.alg, R, C, comm)
+    sh = eng.shard(0)
+    eng.fill_synth()
+    eng.sync()
+
+    for _ in range(args.warmup):
+        eng.multiply()
+    eng.sync()
+
+    eng.kernel_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.multiply()
+    eng.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kt = eng.kernel_ms()
+    eng.kernel_timing(False)
+
+    t = torch.tensor([elapsed, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    # algorithmic bytes: every GPU reads its A shard once, its x segment once, writes its y piece
+    def shard_bytes(s):
+        part = R if args.alg == "colwise" else s.y_len
+        return 8 * (s.n_rows * s.n_cols + s.n_cols + part)
+
+    per_gpu = shard_bytes(sh)
+    total_bytes = sum(shard_bytes(mm.plan_shard(args.alg, R, C, n, r)) for r in range(n))
+    value = total_bytes * args.steps / elapsed / 1e9
+    achieved = per_gpu / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+
+    # quick parity guard on the timed result (rank 0: sampled rows vs the closed form)
+    y = eng.collect()
+
+    # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
+    e2e = None
+    if not args.no_e2e and args.e2e_iters > 0:
+        A = x = None
+        if rank == 0:
+            A = mm.synth_host(R, C, 42)
+            x = mm.synth_host(1, C, 4242)[0]
+            from matvec_mpi_multiplier_amd._lib import lib as _l
+
+            _l.mvg_host_register(A.ctypes.data, A.nbytes)
+        times = []
+        for _ in range(args.e2e_iters):
+            barrier()
+            ts = time.perf_counter()
+            eng.distribute(A, x)
+            eng.multiply()
+            y2 = eng.collect()
+            barrier()
+            tt = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=f"cuda:{local}")
+            if distributed:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            times.append(float(tt[0]))
+        if rank == 0:
+            assert np.array_equal(y2, y), "end-to-end y differs from device-resident y"
+            from matvec_mpi_multiplier_amd._lib import lib as _l
+
+            _l.mvg_host_unregister(A.ctypes.data)
+        e2e = {"mean_s": float(np.mean(times)), "iters": len(times),
+               "GBps": total_bytes / float(np.mean(times)) / 1e9,
+               "semantics": "reference (root holds A, x in host memory; distribute + multiply + y on root)",
+               "distribution": "per-GPU H2D" if not distributed else "root H2D + ncclSend over xGMI"}
+
+    # ---- CPU baseline: rank 0 at N = 1 only
+    cpu = None
+    if rank == 0 and n == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, R, C, y)
+
+    if rank == 0:
+        traffic, traffic_src = pmc_traffic(args.alg, R, C, n)
+        out = {
+            "metric": "fp64 GEMV achieved HBM GB/s per GPU + end-to-end time at 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "GB/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text inputs)",
+            "config": {
+                "workload": f"config 2 weak-scaled: {args.alg} of a ({R} x {C}) fp64 matrix, "
+                            f"{sh.n_rows} x {sh.n_cols} shard per GPU, device-resident",
+                "alg": args.alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
+                "parallelism": f"{args.alg} over {n} GPU(s), exchange "
+                               + {"rowwise": "ncclGather", "colwise": "ncclReduce", "blockwise": "row ncclReduce + leader ncclGather"}[args.alg],
+                "bytes_per_step": total_bytes,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+                "traffic": traffic,
+                "kernel": "gemv_vec (auto variant), per GPU",
+                "kernel_ms": round(kernel_ms, 5),
+                "bytes_per_launch": per_gpu,
+                "traffic_source": traffic_src,
+            },
+            "cpu_baseline": cpu,
+            "end_to_end": e2e,
+        }
+        print(json.dumps(out), flush=True)
+
+    eng.destroy()
+    comm.destroy()
+    if distributed:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, R, C, y_gpu):
+    """The reference's CPU path (oracle restatement, P threads as MPI ranks, distribution
+    from the root's A included, mean of per-iteration max) on this host."""
+    from oracle import oracle
+
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    while R % threads:
+        threads -= 1
+    A = oracle.synth(R, C, 42)
+    x = oracle.synth(1, C, 4242)[0]
+    t1, y_cpu = oracle.time_multiply(args.alg, A, x, threads, 1)
+    iters = max(2, min(200, int(args.cpu_seconds / max(t1, 1e-6))))
+    t, y_cpu = oracle.time_multiply(args.alg, A, x, threads, iters)
+    rel = float(np.max(np.abs(y_gpu - y_cpu) / np.abs(y_cpu)))
+    assert rel <= 1e-12, f"GPU y differs from the reference restatement: {rel}"
+    nbytes = 8 * (R * C + C + R)
+    return {"value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "ms_per_step": round(t * 1e3, 3), "iters": iters,
+            "sample": f"full workload {R}x{C} {args.alg}, {threads} threads as ranks, {iters} iterations "
+                      f"(reference timing semantics: scatter from root + local sums + gather, max over ranks); "
+                      f"GPU y matches to {rel:.1e}",
+            "host_cpu": host_cpu()}
+
+
+def host_cpu():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,32 @@ typedef struct mvg_shard {
 } mvg_shard;
 int mvg_plan_shard(int alg, int64_t R, int64_t C, int nranks, int rank, mvg_shard* out);
 
+/* The exchange step after the local product, as the collective schedule rank `rank` runs
+ * (the engine drives RCCL from exactly this plan; tests replay it over gloo).
+ *   row  : GATHER(world, count = R/P, PART -> Y)                    rowwise.c:141
+ *   col  : REDUCE(world, count = R, PART -> Y)                       colwise.c:124
+ *   block: REDUCE(row comm: color grid_r, key grid_c; count = R/r, PART -> ROW on the leader),
+ *          GATHER(col comm: the grid-column-0 leaders, key grid_r; ROW -> Y)  blockwise.c:144-210
+ *          (one grid row: a single REDUCE straight into Y).
+ * P == 1 has no steps (the product is written straight into Y) unless force_collect != 0.
+ * A communicator is identified by (comm kind, color); ranks order by key; root is the rank
+ * within that communicator (always 0, i.e. world rank 0 / the grid-row leader). */
+#define MVG_X_GATHER    0
+#define MVG_X_REDUCE    1
+#define MVG_X_WORLD     0
+#define MVG_X_ROW       1
+#define MVG_X_COL       2
+#define MVG_X_BUF_PART  0   /* the local product (y_len doubles; R for column split) */
+#define MVG_X_BUF_ROW   1   /* the grid-row sum on the row leader (y_len doubles)       */
+#define MVG_X_BUF_Y     2   /* the full y on world rank 0 (R doubles)                   */
+typedef struct mvg_xstep {
+    int     op, comm, color, key, member, root, src, dst;
+    int64_t count;
+} mvg_xstep;
+#define MVG_MAX_XSTEPS 4
+int mvg_plan_exchange(int alg, int64_t R, int64_t C, int nranks, int rank, int force_collect,
+                      mvg_xstep* steps, int max_steps, int* nsteps);
+
 /* ------------------------------------------------------------------ synthetic inputs
  * value(seed, idx) = (double)k / 10000.0, k = floor(splitmix64(s0 + idx*gamma) * 10000 / 2^64),
  * s0 = splitmix64(seed), gamma = 0x9E3779B97F4A7C15. Every value is exactly what "%.4f" text

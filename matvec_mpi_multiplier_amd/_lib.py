@@ -54,6 +54,24 @@ class Shard(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class XStep(C.Structure):
+    """mvg_xstep: one collective of the exchange schedule (mvg_plan_exchange)."""
+
+    _fields_ = [
+        ("op", C.c_int), ("comm", C.c_int), ("color", C.c_int), ("key", C.c_int),
+        ("member", C.c_int), ("root", C.c_int), ("src", C.c_int), ("dst", C.c_int),
+        ("count", C.c_int64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+X_GATHER, X_REDUCE = 0, 1
+X_WORLD, X_ROW, X_COL = 0, 1, 2
+X_BUF_PART, X_BUF_ROW, X_BUF_Y = 0, 1, 2
+MAX_XSTEPS = 4
+
 _p = C.c_void_p
 _i64 = C.c_int64
 _dp = C.POINTER(C.c_double)
@@ -65,6 +83,8 @@ SIGNATURES = {
     "mvg_last_error": (C.c_char_p, []),
     "mvg_grid_shape": (C.c_int, [_i64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mvg_plan_shard": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.POINTER(Shard)]),
+    "mvg_plan_exchange": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.c_int, C.POINTER(XStep), C.c_int,
+                                     C.POINTER(C.c_int)]),
     "mvg_synth_value": (C.c_double, [C.c_uint64, C.c_uint64]),
     "mvg_synth_fill_host": (C.c_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, C.c_uint64]),
     "mvg_synth_fill_device": (C.c_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, C.c_uint64, _p]),

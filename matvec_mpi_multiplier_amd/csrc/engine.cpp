@@ -65,8 +65,12 @@ struct Shard {
     int device = 0;
     int rank = 0;
     ncclComm_t world = nullptr;
-    ncclComm_t row_comm = nullptr;  // block-split: the c ranks of this grid row
-    ncclComm_t col_comm = nullptr;  // block-split: the r row leaders (grid column 0)
+    // exchange schedule (mvg_plan_exchange) and the communicator each step runs on:
+    // the world, or a split of it (block-split: grid-row comm, grid-column-0 leaders' comm)
+    mvg_xstep steps[MVG_MAX_XSTEPS];
+    int nsteps = 0;
+    ncclComm_t xcomm[MVG_MAX_XSTEPS] = {};
+    bool owns_xcomm[MVG_MAX_XSTEPS] = {};
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;
     double* dA = nullptr;
@@ -127,8 +131,8 @@ void free_shard(Shard& s) {
         (void)hipEventDestroy(ev.second);
     }
     s.ev_pool.clear();
-    if (s.row_comm) (void)ncclCommDestroy(s.row_comm);
-    if (s.col_comm) (void)ncclCommDestroy(s.col_comm);
+    for (int k = 0; k < MVG_MAX_XSTEPS; ++k)
+        if (s.owns_xcomm[k] && s.xcomm[k]) (void)ncclCommDestroy(s.xcomm[k]);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.copy_stream) (void)hipStreamDestroy(s.copy_stream);
     s = Shard{};
@@ -273,33 +277,36 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         if ((rc = alloc_doubles(&s.dx, x_len(p))) != MVG_OK) return bail(rc);
         const int64_t part = alg == MVG_ALG_COLWISE ? R : p.y_len;
         if ((rc = alloc_doubles(&s.dy_part, part)) != MVG_OK) return bail(rc);
-        if (alg == MVG_ALG_BLOCKWISE && p.grid_c == 0 && p.grid_rows > 1)
+        if ((rc = mvg_plan_exchange(alg, R, C, comm->nranks, l.rank, e->always_collect, s.steps,
+                                    MVG_MAX_XSTEPS, &s.nsteps)) != MVG_OK)
+            return bail(rc);
+        bool need_row = false;
+        for (int k = 0; k < s.nsteps; ++k)
+            need_row |= s.steps[k].member && (s.steps[k].dst == MVG_X_BUF_ROW || s.steps[k].src == MVG_X_BUF_ROW);
+        if (need_row)
             if ((rc = alloc_doubles(&s.dy_row, p.y_len)) != MVG_OK) return bail(rc);
         if (l.rank == 0)
             if ((rc = alloc_doubles(&s.dy, R)) != MVG_OK) return bail(rc);
     }
-    // Block-split sub-communicators: ncclCommSplit is collective over the world, so every
-    // local rank calls it inside one group.
-    if (alg == MVG_ALG_BLOCKWISE && comm->nranks > 1) {
+    // Sub-communicators of the exchange schedule. ncclCommSplit is collective over the world,
+    // so every local rank calls it for every split step, inside one group per step.
+    const int nsteps = e->shards[0].nsteps;
+    for (int k = 0; k < nsteps; ++k) {
+        if (e->shards[0].steps[k].comm == MVG_X_WORLD) {
+            for (auto& s : e->shards) s.xcomm[k] = s.world;
+            continue;
+        }
         ncclResult_t r = ncclGroupStart();
         for (auto& s : e->shards) {
             if (r != ncclSuccess) break;
             (void)hipSetDevice(s.device);
-            r = ncclCommSplit(s.world, s.plan.grid_r, s.plan.grid_c, &s.row_comm, nullptr);
+            const mvg_xstep& st = s.steps[k];
+            r = ncclCommSplit(s.world, st.member ? st.color : NCCL_SPLIT_NOCOLOR, st.key, &s.xcomm[k], nullptr);
+            s.owns_xcomm[k] = true;
         }
         ncclResult_t r2 = ncclGroupEnd();
-        if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit(row)"));
-        if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit(row) group"));
-        r = ncclGroupStart();
-        for (auto& s : e->shards) {
-            if (r != ncclSuccess) break;
-            (void)hipSetDevice(s.device);
-            const int color = s.plan.grid_c == 0 ? 0 : NCCL_SPLIT_NOCOLOR;
-            r = ncclCommSplit(s.world, color, s.plan.grid_r, &s.col_comm, nullptr);
-        }
-        r2 = ncclGroupEnd();
-        if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit(col)"));
-        if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit(col) group"));
+        if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit"));
+        if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit group"));
     }
     *out = e;
     return MVG_OK;
@@ -451,7 +458,8 @@ int mvg_engine_multiply(mvg_engine* e) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
     if (!e->distributed) return fail(MVG_E_STATE, "mvg_engine_multiply before distribute/fill");
     DeviceGuard g;
-    const bool solo = e->nranks == 1 && !e->always_collect;
+    const int nsteps = e->shards[0].nsteps;
+    const bool solo = nsteps == 0;  // P == 1: the product goes straight into y
     // 1) local product on every device
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
@@ -474,44 +482,24 @@ int mvg_engine_multiply(mvg_engine* e) {
         if (rc != MVG_OK) return rc;
         if (e->timing) MVG_HIP(hipEventRecord(t1, s.stream));
     }
-    if (solo) return MVG_OK;
-    // 2) the exchange step
-    if (e->alg == MVG_ALG_ROWWISE) {
+    // 2) the exchange step, from the shared schedule (mvg_plan_exchange)
+    for (int k = 0; k < nsteps; ++k) {
         MVG_NCCL(ncclGroupStart());
         for (auto& s : e->shards) {
+            const mvg_xstep& st = s.steps[k];
+            if (!st.member) continue;
             (void)hipSetDevice(s.device);
-            MVG_NCCL(ncclGather(s.dy_part, s.dy ? s.dy : s.dy_part, (size_t)s.plan.y_len, ncclFloat64, 0, s.world, s.stream));
-        }
-        MVG_NCCL(ncclGroupEnd());
-    } else if (e->alg == MVG_ALG_COLWISE) {
-        MVG_NCCL(ncclGroupStart());
-        for (auto& s : e->shards) {
-            (void)hipSetDevice(s.device);
-            MVG_NCCL(ncclReduce(s.dy_part, s.dy ? s.dy : s.dy_part, (size_t)e->R, ncclFloat64, ncclSum, 0, s.world, s.stream));
-        }
-        MVG_NCCL(ncclGroupEnd());
-    } else {
-        const bool one_row = e->shards[0].plan.grid_rows == 1;
-        // row reduce to the grid-row leader; with a single grid row the leader is the root
-        // and reduces straight into y.
-        MVG_NCCL(ncclGroupStart());
-        for (auto& s : e->shards) {
-            (void)hipSetDevice(s.device);
-            ncclComm_t rc = s.row_comm ? s.row_comm : s.world;
-            double* dst = one_row ? s.dy : s.dy_row;
-            if (!dst) dst = s.dy_part;  // recvbuff is only used on the root
-            MVG_NCCL(ncclReduce(s.dy_part, dst, (size_t)s.plan.y_len, ncclFloat64, ncclSum, 0, rc, s.stream));
-        }
-        MVG_NCCL(ncclGroupEnd());
-        if (!one_row) {
-            MVG_NCCL(ncclGroupStart());
-            for (auto& s : e->shards) {
-                if (!s.col_comm) continue;
-                (void)hipSetDevice(s.device);
-                MVG_NCCL(ncclGather(s.dy_row, s.dy, (size_t)s.plan.y_len, ncclFloat64, 0, s.col_comm, s.stream));
+            double* bufs[3] = {s.dy_part, s.dy_row, s.dy};
+            const double* src = bufs[st.src];
+            double* dst = bufs[st.dst];
+            if (!dst) dst = s.dy_part;  // recvbuff is only written on the root
+            if (st.op == MVG_X_GATHER) {
+                MVG_NCCL(ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], s.stream));
+            } else {
+                MVG_NCCL(ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], s.stream));
             }
-            MVG_NCCL(ncclGroupEnd());
         }
+        MVG_NCCL(ncclGroupEnd());
     }
     return MVG_OK;
 }

@@ -164,6 +164,59 @@ int mvg_plan_shard(int alg, int64_t R, int64_t C, int P, int rank, mvg_shard* o)
     }
 }
 
+int mvg_plan_exchange(int alg, int64_t R, int64_t C, int P, int rank, int force,
+                      mvg_xstep* steps, int max_steps, int* nsteps) {
+    if (!steps || !nsteps || max_steps < 0) return fail(MVG_E_INVALID, "mvg_plan_exchange: null");
+    *nsteps = 0;
+    mvg_shard s;
+    int rc = mvg_plan_shard(alg, R, C, P, rank, &s);
+    if (rc != MVG_OK) return rc;
+    if (P == 1 && !force) return MVG_OK;
+    mvg_xstep v[2];
+    int n = 0;
+    memset(v, 0, sizeof v);
+    if (alg == MVG_ALG_ROWWISE || alg == MVG_ALG_COLWISE) {
+        v[0].op = alg == MVG_ALG_ROWWISE ? MVG_X_GATHER : MVG_X_REDUCE;
+        v[0].comm = MVG_X_WORLD;
+        v[0].color = 0;
+        v[0].key = rank;
+        v[0].member = 1;
+        v[0].root = 0;
+        v[0].src = MVG_X_BUF_PART;
+        v[0].dst = MVG_X_BUF_Y;
+        v[0].count = s.y_len;
+        n = 1;
+    } else {
+        const bool one_row = s.grid_rows == 1;
+        v[0].op = MVG_X_REDUCE;
+        v[0].comm = MVG_X_ROW;
+        v[0].color = s.grid_r;
+        v[0].key = s.grid_c;
+        v[0].member = 1;
+        v[0].root = 0;
+        v[0].src = MVG_X_BUF_PART;
+        v[0].dst = one_row ? MVG_X_BUF_Y : MVG_X_BUF_ROW;
+        v[0].count = s.y_len;
+        n = 1;
+        if (!one_row) {
+            v[1].op = MVG_X_GATHER;
+            v[1].comm = MVG_X_COL;
+            v[1].color = 0;
+            v[1].key = s.grid_r;
+            v[1].member = s.grid_c == 0;
+            v[1].root = 0;
+            v[1].src = MVG_X_BUF_ROW;
+            v[1].dst = MVG_X_BUF_Y;
+            v[1].count = s.y_len;
+            n = 2;
+        }
+    }
+    if (n > max_steps) return fail(MVG_E_INVALID, "mvg_plan_exchange: steps buffer too small");
+    for (int i = 0; i < n; ++i) steps[i] = v[i];
+    *nsteps = n;
+    return MVG_OK;
+}
+
 // ------------------------------------------------------------------ synthetic (host)
 double mvg_synth_value(uint64_t seed, uint64_t idx) { return synth_value(splitmix64(seed), idx); }
 

@@ -18,6 +18,7 @@
  *     them in MPI_ANY_SOURCE arrival order (nondeterministic); this oracle uses rank order.
  * Sizes are 64-bit throughout (the reference's int counts overflow at the large configs).
  */
+#define _GNU_SOURCE
 #include "cpu_ref.h"
 
 #include <pthread.h>
@@ -151,6 +152,13 @@ double ref_synth_value(uint64_t seed, uint64_t idx) {
 void ref_synth_fill(double* dst, int64_t R, int64_t C, uint64_t seed) {
     for (int64_t i = 0; i < R; ++i)
         for (int64_t j = 0; j < C; ++j) dst[i * C + j] = ref_synth_value(seed, (uint64_t)(i * C + j));
+}
+
+/* rows [r0, r0+nr) x cols [c0, c0+nc) of a global matrix with C columns, packed (ld = nc) */
+void ref_synth_block(double* dst, int64_t r0, int64_t nr, int64_t c0, int64_t nc, int64_t C, uint64_t seed) {
+    for (int64_t i = 0; i < nr; ++i)
+        for (int64_t j = 0; j < nc; ++j)
+            dst[i * nc + j] = ref_synth_value(seed, (uint64_t)((r0 + i) * C + c0 + j));
 }
 
 /* ---------------------------------------------------------------- CPU baseline timing

@@ -13,6 +13,7 @@ int ref_blockwise(const double* A, const double* x, int64_t R, int64_t C, int P,
 int ref_multiply(int alg, const double* A, const double* x, int64_t R, int64_t C, int P, double* y);
 double ref_synth_value(uint64_t seed, uint64_t idx);
 void ref_synth_fill(double* dst, int64_t R, int64_t C, uint64_t seed);
+void ref_synth_block(double* dst, int64_t r0, int64_t nr, int64_t c0, int64_t nc, int64_t C, uint64_t seed);
 double ref_time_multiply(int alg, const double* A, const double* x, int64_t R, int64_t C, int P,
                          int iters, double* y);
 

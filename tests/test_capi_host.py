@@ -1,0 +1,231 @@
+"""C-ABI library: loads, exports every declared symbol, and its host-only logic (planner,
+exchange schedule, synthetic generator, text I/O) matches the reference's behaviour. No GPU."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DIR, REPO
+from matvec_mpi_multiplier_amd import _lib
+from matvec_mpi_multiplier_amd import multiplier as mm
+from oracle import oracle
+
+HEADER = os.path.join(REPO, "include", "matvec_gpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mvg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 40
+    lib = C.CDLL(_lib.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes binding covers the whole header
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+
+
+def test_built_for_gfx950():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version_and_errors():
+    assert b"gfx950" in _lib.lib.mvg_version()
+    assert _lib.lib.mvg_strerror(_lib.MVG_E_INDIVISIBLE) == b"shape does not divide over the rank count"
+    rc = _lib.lib.mvg_plan_shard(0, 10, 10, 3, 0, C.byref(_lib.Shard()))
+    assert rc == _lib.MVG_E_INDIVISIBLE
+    assert b"10 mod 3 = 1. Unable to parallellize task." == _lib.lib.mvg_last_error()
+
+
+@pytest.mark.parametrize("p", list(range(1, 130)))
+def test_grid_shape_matches_reference(p):
+    assert mm.get_2_most_closest_multipliers(p) == oracle.grid_shape(p)
+
+
+def test_grid_shape_rejects_nonpositive():
+    with pytest.raises(_lib.MvgError):
+        mm.get_2_most_closest_multipliers(0)
+
+
+# ---------------------------------------------------------------- shard planner
+def _tiles(alg, R, Cn, P):
+    return [mm.plan_shard(alg, R, Cn, P, r) for r in range(P)]
+
+
+@pytest.mark.parametrize("R,Cn,P", [(4, 8, 2), (480, 480, 6), (120, 6000, 8), (960, 96, 3), (16384, 16384, 8),
+                                    (4194304, 512, 8), (131072, 131072, 8), (65536, 65536, 8)])
+def test_shards_tile_the_matrix(R, Cn, P):
+    for alg in ("rowwise", "colwise", "blockwise"):
+        try:
+            shards = _tiles(alg, R, Cn, P)
+        except _lib.IndivisibleError:
+            continue
+        cover = sum(s.n_rows * s.n_cols for s in shards)
+        assert cover == R * Cn
+        # disjoint: distinct (row_off, col_off) origins on a regular grid
+        assert len({(s.row_off, s.col_off) for s in shards}) == P
+        for s in shards:
+            assert 0 <= s.row_off and s.row_off + s.n_rows <= R
+            assert 0 <= s.col_off and s.col_off + s.n_cols <= Cn
+
+
+def test_rowwise_plan_is_scatter_order():
+    s = _tiles("rowwise", 12, 5, 3)
+    assert [(t.row_off, t.n_rows, t.col_off, t.n_cols, t.y_off, t.y_len) for t in s] == [
+        (0, 4, 0, 5, 0, 4), (4, 4, 0, 5, 4, 4), (8, 4, 0, 5, 8, 4)]
+
+
+def test_colwise_plan_is_strip_order():
+    s = _tiles("colwise", 3, 12, 4)
+    assert [(t.col_off, t.n_cols, t.n_rows, t.y_len) for t in s] == [(0, 3, 3, 3), (3, 3, 3, 3), (6, 3, 3, 3), (9, 3, 3, 3)]
+
+
+def test_blockwise_plan_is_rank_i_times_c_plus_j():
+    # multiplier_blockwise.c:56,71: block (i, j) goes to rank i*c + j on the r x c grid
+    s = _tiles("blockwise", 8, 12, 8)  # 2 x 4 grid
+    for t in s:
+        assert (t.grid_rows, t.grid_cols) == (2, 4)
+        assert t.rank == t.grid_r * 4 + t.grid_c
+        assert (t.row_off, t.col_off, t.n_rows, t.n_cols) == (t.grid_r * 4, t.grid_c * 3, 4, 3)
+
+
+def test_divisibility_errors_match_reference_checks():
+    # rowwise.c:72 R % P; colwise.c:151 C % P; blockwise.c:278 (R*C) % P
+    with pytest.raises(_lib.IndivisibleError):
+        mm.plan_shard("rowwise", 10, 8, 4, 0)
+    mm.plan_shard("rowwise", 12, 7, 4, 0)
+    with pytest.raises(_lib.IndivisibleError):
+        mm.plan_shard("colwise", 8, 10, 4, 0)
+    mm.plan_shard("colwise", 7, 12, 4, 0)
+    with pytest.raises(_lib.IndivisibleError):
+        mm.plan_shard("blockwise", 5, 5, 2, 0)
+
+
+def test_blockwise_refuses_ragged_grid_the_reference_truncates():
+    # 3 x 8 at P=4 passes the reference's (R*C) % P check but R % 2 != 0: the reference drops
+    # a row (SURVEY §4 bug 1); the planner refuses (deliberate deviation).
+    with pytest.raises(_lib.IndivisibleError):
+        mm.plan_shard("blockwise", 3, 8, 4, 0)
+    with pytest.raises(_lib.IndivisibleError):
+        mm.plan_shard("blockwise", 4, 5, 4, 0)
+
+
+def test_plan_rejects_bad_arguments():
+    for args in [(0, 4, 4, 0, 0), (0, 4, 4, 2, 2), (0, -1, 4, 1, 0), (9, 4, 4, 1, 0)]:
+        with pytest.raises(_lib.MvgError):
+            mm.plan_shard(*args)
+
+
+def test_empty_shapes_plan():
+    s = mm.plan_shard("rowwise", 0, 5, 2, 1)
+    assert s.n_rows == 0
+    assert mm.plan_shard("colwise", 3, 0, 1, 0).n_cols == 0
+
+
+# ---------------------------------------------------------------- exchange schedule
+def test_exchange_rowwise_and_colwise():
+    for r in range(4):
+        (st,) = mm.plan_exchange("rowwise", 16, 8, 4, r)
+        assert (st.op, st.comm, st.member, st.root, st.count, st.src, st.dst) == (
+            _lib.X_GATHER, _lib.X_WORLD, 1, 0, 4, _lib.X_BUF_PART, _lib.X_BUF_Y)
+        (st,) = mm.plan_exchange("colwise", 16, 8, 4, r)
+        assert (st.op, st.comm, st.count) == (_lib.X_REDUCE, _lib.X_WORLD, 16)
+
+
+def test_exchange_blockwise_two_level():
+    for r in range(8):  # 2 x 4 grid
+        red, gat = mm.plan_exchange("blockwise", 16, 16, 8, r)
+        gi, gj = divmod(r, 4)
+        assert (red.op, red.comm, red.color, red.key, red.member, red.count) == (_lib.X_REDUCE, _lib.X_ROW, gi, gj, 1, 8)
+        assert red.dst == _lib.X_BUF_ROW
+        assert (gat.op, gat.comm, gat.key, gat.member, gat.src, gat.dst) == (
+            _lib.X_GATHER, _lib.X_COL, gi, int(gj == 0), _lib.X_BUF_ROW, _lib.X_BUF_Y)
+
+
+def test_exchange_blockwise_single_grid_row_reduces_into_y():
+    for r in range(3):  # 1 x 3 grid
+        (red,) = mm.plan_exchange("blockwise", 6, 9, 3, r)
+        assert red.comm == _lib.X_ROW and red.dst == _lib.X_BUF_Y
+
+
+def test_exchange_solo_has_no_steps_unless_forced():
+    for alg in ("rowwise", "colwise", "blockwise"):
+        assert mm.plan_exchange(alg, 8, 8, 1, 0) == []
+        assert len(mm.plan_exchange(alg, 8, 8, 1, 0, force_collect=True)) == 1
+
+
+# ---------------------------------------------------------------- synthetic generator
+def test_synth_host_matches_oracle_bit_exact():
+    A = mm.synth_host(37, 129, 42)
+    np.testing.assert_array_equal(A, oracle.synth(37, 129, 42))
+    blk = oracle.synth_block(5, 7, 100, 29, 129, 42)
+    np.testing.assert_array_equal(A[5:12, 100:129], blk)
+    assert _lib.lib.mvg_synth_value(4242, 17) == oracle.synth_value(4242, 17)
+
+
+def test_synth_large_index_matches_oracle():
+    for idx in (0, 1, 2**32 - 1, 2**32 + 7, 131072 * 131072 - 1, 2**62 + 3):
+        assert _lib.lib.mvg_synth_value(42, idx) == oracle.synth_value(42, idx)
+
+
+# ---------------------------------------------------------------- text I/O
+def test_filenames_match_reference():
+    assert mm.build_matrix_filename(4, 8) == "matrix_4_8.txt"
+    assert mm.build_vector_filename(8) == "vector_8.txt"
+    assert mm.build_matrix_filename(131072, 131072) == "matrix_131072_131072.txt"
+
+
+def test_load_reference_fixture():
+    A = mm.load_matr(4, 8, GOLDEN_DIR)
+    x = mm.load_vec(8, GOLDEN_DIR)
+    np.testing.assert_array_equal(A, np.loadtxt(os.path.join(GOLDEN_DIR, "matrix_4_8.txt")))
+    np.testing.assert_array_equal(x, np.arange(1, 9, dtype=np.float64))
+
+
+def test_missing_file_is_io_error(tmp_path):
+    with pytest.raises(_lib.MvgError) as e:
+        mm.load_matr(3, 3, str(tmp_path))
+    assert e.value.code == _lib.MVG_E_IO
+
+
+def test_short_file_is_io_error(tmp_path):
+    (tmp_path / "vector_5.txt").write_text("1.0 2.0 3.0\n")
+    with pytest.raises(_lib.MvgError) as e:
+        mm.load_vec(5, str(tmp_path))
+    assert e.value.code == _lib.MVG_E_IO
+
+
+def test_non_numeric_token_is_io_error(tmp_path):
+    (tmp_path / "vector_3.txt").write_text("1.0 abc 3.0\n")
+    with pytest.raises(_lib.MvgError):
+        mm.load_vec(3, str(tmp_path))
+
+
+def test_free_form_whitespace_and_extra_tokens(tmp_path):
+    # fscanf("%lf") reads whitespace-separated tokens regardless of line layout and stops
+    # after R*C values (matr_utils.c:55-59)
+    (tmp_path / "matrix_2_3.txt").write_text("  1.5\t2.25\n\n3e-1 4\r\n5.0000 -6.125 99 100\n")
+    A = mm.load_matr(2, 3, str(tmp_path))
+    np.testing.assert_array_equal(A, [[1.5, 2.25, 0.3], [4.0, 5.0, -6.125]])
+
+
+def test_synth_text_roundtrip_parallel_parser(tmp_path):
+    # > 1 MiB so the parser splits the file over threads; bit-exact vs the generator
+    R, Cn = 300, 700
+    mm.write_matr_synth(str(tmp_path / f"matrix_{R}_{Cn}.txt"), R, Cn, 42)
+    A = mm.load_matr(R, Cn, str(tmp_path))
+    np.testing.assert_array_equal(A, oracle.synth(R, Cn, 42))
+    np.testing.assert_array_equal(A, np.loadtxt(tmp_path / f"matrix_{R}_{Cn}.txt"))
+
+
+def test_write_vec_roundtrips(tmp_path):
+    v = np.array([222.19999999999999, 1e-300, -0.0, 3.141592653589793, 1076.4842229100022])
+    mm.write_vec(str(tmp_path / "vector_5.txt"), v)
+    np.testing.assert_array_equal(mm.load_vec(5, str(tmp_path)), v)
