@@ -58,7 +58,7 @@ def log(*a):
 def pmc_traffic(alg: str, R: int, C: int, n: int):
     """HBM bytes per GEMV launch from the committed rocprofv3 PMC summary for this config
     (profiles/*pmc*.json written by tools/pmc_traffic.py), or None."""
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(path))
         except Exception:

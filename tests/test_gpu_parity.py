@@ -105,10 +105,10 @@ def test_device_synth_fill_bit_exact():
     np.testing.assert_array_equal(d.download().reshape(R, Cn), oracle.synth(R, Cn, 42))
     # a shard of a huge global matrix (64-bit global index)
     GC = 131072
-    _lib.check(_lib.lib.mvg_synth_fill_device(d.ptr, 100, 50, 100, 70000, 131000, GC, 42, None), "fill")
+    _lib.check(_lib.lib.mvg_synth_fill_device(d.ptr, 100, 50, 100, 70000, 130900, GC, 42, None), "fill")
     _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
     got = d.download(50 * 100).reshape(50, 100)
-    np.testing.assert_array_equal(got, oracle.synth_block(70000, 50, 131000, 100, GC, 42))
+    np.testing.assert_array_equal(got, oracle.synth_block(70000, 50, 130900, 100, GC, 42))
 
 
 # ---------------------------------------------------------------- engine vs golden (P = 1)
