@@ -1,0 +1,134 @@
+"""The N > 1 path on CPU: world_size 2 and 4 over torch.distributed `gloo`.
+
+Each rank takes its shard from the C planner (mvg_plan_shard), computes its local product
+(with the oracle standing in for the GPU kernel — there is no GPU here), then runs the exchange
+step exactly as the C engine does: the same schedule from mvg_plan_exchange (gather / reduce,
+world / grid-row / leader communicators, buffers, roots), executed with gloo collectives instead
+of RCCL. Rank 0's y must equal the reference's golden y at that P. Also covers the 128-byte
+RCCL unique-id bootstrap that bench.py runs over the default process group.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN_DIR, REPO, max_rel
+
+CASES = [
+    # (case, R, C, alg, P, exact)
+    ("fixture_4x8", 4, 8, "rowwise", 2, True),
+    ("fixture_4x8", 4, 8, "colwise", 2, True),
+    ("fixture_4x8", 4, 8, "blockwise", 2, True),
+    ("fixture_4x8", 4, 8, "rowwise", 4, True),
+    ("fixture_4x8", 4, 8, "colwise", 4, False),
+    ("fixture_4x8", 4, 8, "blockwise", 4, True),
+    ("sq_480", 480, 480, "rowwise", 2, True),
+    ("sq_480", 480, 480, "colwise", 2, True),
+    ("sq_480", 480, 480, "blockwise", 2, True),
+    ("sq_480", 480, 480, "colwise", 4, False),
+    ("sq_480", 480, 480, "blockwise", 4, True),
+    ("wide_120x6000", 120, 6000, "blockwise", 4, True),
+    ("tall_960x96", 960, 96, "rowwise", 4, True),
+]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs(case, R, C):
+    from oracle import oracle
+
+    if case.startswith("fixture"):
+        A = np.loadtxt(os.path.join(GOLDEN_DIR, "matrix_4_8.txt")).reshape(4, 8)
+        x = np.loadtxt(os.path.join(GOLDEN_DIR, "vector_8.txt"))
+        return A, x
+    return oracle.synth(R, C, 42), oracle.synth(1, C, 4242)[0]
+
+
+def _worker(rank, world, port, case, R, C, alg, outq):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd import _lib
+    from matvec_mpi_multiplier_amd import multiplier as mm
+    from oracle import oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # --- bootstrap: rank 0's 128-byte id reaches every rank unchanged
+        fake = bytes((i * 7 + 3) % 256 for i in range(_lib.UNIQUE_ID_BYTES))
+        uid = mm.broadcast_unique_id(lambda: fake)
+        assert uid == fake
+
+        # --- local product on this rank's shard
+        A, x = _inputs(case, R, C)
+        s = mm.plan_shard(alg, R, C, world, rank)
+        blk = A[s.row_off:s.row_off + s.n_rows, s.col_off:s.col_off + s.n_cols]
+        part = oracle.multiply_std_rowwise(blk, x[s.col_off:s.col_off + s.n_cols])
+        bufs = {_lib.X_BUF_PART: torch.from_numpy(part.copy()),
+                _lib.X_BUF_ROW: torch.zeros(s.y_len, dtype=torch.float64),
+                _lib.X_BUF_Y: torch.zeros(R, dtype=torch.float64)}
+
+        # --- the exchange schedule, as the C engine runs it over RCCL
+        plans = [mm.plan_exchange(alg, R, C, world, r) for r in range(world)]
+        nsteps = len(plans[rank])
+        assert all(len(p) == nsteps for p in plans)
+        for k in range(nsteps):
+            st = plans[rank][k]
+            # communicator = members of this step with the same color, ordered by key
+            groups = {}
+            for r in range(world):
+                o = plans[r][k]
+                if o.member:
+                    groups.setdefault(o.color, []).append((o.key, r))
+            handles = {}
+            for color in sorted(groups):  # every rank creates every group, same order
+                ranks = [r for _, r in sorted(groups[color])]
+                handles[color] = (ranks, dist.new_group(ranks) if st.comm != _lib.X_WORLD else None)
+            if not st.member:
+                continue
+            ranks, g = handles[st.color]
+            root = ranks[st.root]
+            src = bufs[st.src]
+            assert src.numel() == st.count
+            if st.op == _lib.X_GATHER:
+                gl = [torch.empty(st.count, dtype=torch.float64) for _ in ranks] if rank == root else None
+                dist.gather(src, gather_list=gl, dst=root, group=g)
+                if rank == root:
+                    bufs[st.dst][: st.count * len(ranks)] = torch.cat(gl)
+            else:
+                t = src.clone()
+                dist.reduce(t, dst=root, op=dist.ReduceOp.SUM, group=g)
+                if rank == root:
+                    bufs[st.dst][: st.count] = t
+        if rank == 0:
+            outq.put(bufs[_lib.X_BUF_Y].numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,R,C,alg,P,exact", CASES)
+def test_gloo_exchange_replay_matches_reference(golden, case, R, C, alg, P, exact):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, P, port, case, R, C, alg, q)) for r in range(P)]
+    for p in procs:
+        p.start()
+    y = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = golden[f"{case}/{alg}/P{P}"]
+    if exact:
+        np.testing.assert_array_equal(y, want)
+    else:  # gloo's reduce order for > 2 ranks is its own (MPICH/RCCL differ too)
+        assert max_rel(y, want) <= 1e-15
