@@ -51,8 +51,35 @@ __device__ __forceinline__ double group_sum(double v) {
 
 constexpr int kBlock = 256;  // 4 waves
 
+// Options of the 16-B kernel (template bit mask).
+constexpr int kPipe = 1;     // software pipeline: chunk i+1's loads issue before chunk i's FMAs
+constexpr int kStagger = 2;  // each wave starts at its own column chunk and wraps around, so the
+                             // waves in flight read spread-out columns instead of all the same one
+
+template <int RPG, int UNR, bool NT>
+__device__ __forceinline__ void load_chunk(const double* const (&arow)[RPG], const double* x, int64_t base,
+                                           int64_t step, dbl2 (&xv)[UNR], dbl2 (&av)[RPG][UNR]) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) xv[u] = load2<false>(x + base + u * step);
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) av[r][u] = load2<NT>(arow[r] + base + u * step);
+}
+
+template <int RPG, int UNR>
+__device__ __forceinline__ void fma_chunk(double (&acc)[RPG], const dbl2 (&xv)[UNR], const dbl2 (&av)[RPG][UNR]) {
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            acc[r] = __builtin_fma(av[r][u].x, xv[u].x, acc[r]);
+            acc[r] = __builtin_fma(av[r][u].y, xv[u].y, acc[r]);
+        }
+}
+
 // 16-B path. Requires lda even, A and x 16-B aligned.
-template <int LPR, int RPG, int UNR, bool NT>
+template <int LPR, int RPG, int UNR, bool NT, int OPT>
 __global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ x,
                                                    double* __restrict__ y, int64_t M,
@@ -77,25 +104,44 @@ __global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A,
 
     constexpr int64_t kStep = 2 * LPR;        // columns one group covers per sub-step
     constexpr int64_t kChunk = kStep * UNR;   // columns per iteration
-    const int64_t kmain = (K / kChunk) * kChunk;
+    const int64_t nch = K / kChunk;
+    const int64_t kmain = nch * kChunk;
     const int64_t c0 = 2 * gl;
+    int64_t start = 0;
+    if constexpr ((OPT & kStagger) != 0) start = nch > 0 ? (wave * 5) % nch : 0;
+    auto chunk_base = [&](int64_t i) {
+        int64_t c = start + i;
+        if (c >= nch) c -= nch;
+        return c * kChunk + c0;
+    };
 
-    for (int64_t base = c0; base < kmain; base += kChunk) {
-        dbl2 xv[UNR];
-        dbl2 av[RPG][UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) xv[u] = load2<false>(x + base + u * kStep);
-#pragma unroll
-        for (int r = 0; r < RPG; ++r)
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) av[r][u] = load2<NT>(arow[r] + base + u * kStep);
-#pragma unroll
-        for (int r = 0; r < RPG; ++r)
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                acc[r] = __builtin_fma(av[r][u].x, xv[u].x, acc[r]);
-                acc[r] = __builtin_fma(av[r][u].y, xv[u].y, acc[r]);
+    if constexpr ((OPT & kPipe) != 0) {
+        if (nch > 0) {
+            dbl2 xa[UNR], xb[UNR];
+            dbl2 aa[RPG][UNR], ab[RPG][UNR];
+            load_chunk<RPG, UNR, NT>(arow, x, chunk_base(0), kStep, xa, aa);
+            int64_t i = 1;
+            for (; i + 1 < nch; i += 2) {
+                load_chunk<RPG, UNR, NT>(arow, x, chunk_base(i), kStep, xb, ab);
+                fma_chunk<RPG, UNR>(acc, xa, aa);
+                load_chunk<RPG, UNR, NT>(arow, x, chunk_base(i + 1), kStep, xa, aa);
+                fma_chunk<RPG, UNR>(acc, xb, ab);
             }
+            if (i < nch) {
+                load_chunk<RPG, UNR, NT>(arow, x, chunk_base(i), kStep, xb, ab);
+                fma_chunk<RPG, UNR>(acc, xa, aa);
+                fma_chunk<RPG, UNR>(acc, xb, ab);
+            } else {
+                fma_chunk<RPG, UNR>(acc, xa, aa);
+            }
+        }
+    } else {
+        for (int64_t i = 0; i < nch; ++i) {
+            dbl2 xv[UNR];
+            dbl2 av[RPG][UNR];
+            load_chunk<RPG, UNR, NT>(arow, x, chunk_base(i), kStep, xv, av);
+            fma_chunk<RPG, UNR>(acc, xv, av);
+        }
     }
     // column tail: whole pairs, then a possible last odd column
     for (int64_t c = kmain + c0; c < K; c += kStep) {
@@ -117,6 +163,86 @@ __global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A,
     for (int r = 0; r < RPG; ++r) {
         const double s = group_sum<LPR>(acc[r]);
         if (gl == 0 && row0 + r < M) y[row0 + r] = s;
+    }
+}
+
+// Row-per-workgroup 16-B path: workgroup b (NW waves) owns rows [b*RPB, +RPB); wave w takes
+// column chunks w, w+NW, w+2NW, ... of every such row (a chunk = 64 lanes x UNR x 16 B), so the
+// workgroup sweeps its rows front to back and consecutive workgroups - which the dispatcher
+// keeps resident together - read consecutive memory: the chip streams a sliding window of A
+// instead of thousands of scattered row positions. Per-wave partial sums meet in LDS and are
+// added in wave order (fixed, deterministic). Pipelined: chunk i+NW's loads issue before
+// chunk i's FMAs.
+template <int NW, int RPB, int UNR, bool NT>
+__global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
+                                                         const double* __restrict__ x,
+                                                         double* __restrict__ y, int64_t M,
+                                                         int64_t K) {
+    __shared__ double part[NW][RPB];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t row0 = (int64_t)blockIdx.x * RPB;
+    const double* arow[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    double acc[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) acc[r] = 0.0;
+
+    constexpr int64_t kStep = 128;            // columns per wave per sub-step (64 lanes x 2)
+    constexpr int64_t kChunk = kStep * UNR;
+    const int64_t nch = K / kChunk;
+    const int64_t c0 = 2 * lane;
+    int64_t i = w;
+    if (i < nch) {
+        dbl2 xa[UNR], xb[UNR];
+        dbl2 aa[RPB][UNR], ab[RPB][UNR];
+        load_chunk<RPB, UNR, NT>(arow, x, i * kChunk + c0, kStep, xa, aa);
+        for (; i + NW < nch; i += 2 * NW) {
+            load_chunk<RPB, UNR, NT>(arow, x, (i + NW) * kChunk + c0, kStep, xb, ab);
+            fma_chunk<RPB, UNR>(acc, xa, aa);
+            if (i + 2 * NW < nch) {
+                load_chunk<RPB, UNR, NT>(arow, x, (i + 2 * NW) * kChunk + c0, kStep, xa, aa);
+                fma_chunk<RPB, UNR>(acc, xb, ab);
+            } else {
+                fma_chunk<RPB, UNR>(acc, xb, ab);
+                i = nch;  // both buffers consumed
+                break;
+            }
+        }
+        if (i < nch) fma_chunk<RPB, UNR>(acc, xa, aa);
+    }
+    // column tail (K % kChunk), spread over the whole workgroup
+    for (int64_t c = nch * kChunk + 2 * (int64_t)threadIdx.x; c < K; c += 2 * NW * 64) {
+        if (c + 1 < K) {
+            const dbl2 xv = load2<false>(x + c);
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) {
+                const dbl2 a = load2<NT>(arow[r] + c);
+                acc[r] = __builtin_fma(a.x, xv.x, acc[r]);
+                acc[r] = __builtin_fma(a.y, xv.y, acc[r]);
+            }
+        } else {
+            const double xs = x[c];
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) acc[r] = __builtin_fma(arow[r][c], xs, acc[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        const double s = group_sum<64>(acc[r]);
+        if (lane == 0) part[w][r] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < RPB && row0 + threadIdx.x < M) {
+        double s = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += part[v][threadIdx.x];
+        y[row0 + threadIdx.x] = s;
     }
 }
 
@@ -179,51 +305,67 @@ typedef void (*gemv_fn)(const double*, int64_t, const double*, double*, int64_t,
 struct Variant {
     const char* name;
     gemv_fn fn;
-    int rows_per_wave;  // G * RPG
-    bool vec;           // needs 16-B alignment + even lda
+    int rows_per_block;  // rows one workgroup covers
+    bool vec;            // needs 16-B alignment + even lda
+    int threads;         // workgroup size
 };
 
-#define VEC(LPR, RPG, UNR, NT) \
-    {"vec_l" #LPR "_r" #RPG "_u" #UNR "_nt" #NT, gemv_vec<LPR, RPG, UNR, NT>, (64 / LPR) * RPG, true}
-#define SCL(LPR, RPG, UNR, NT) \
-    {"scl_l" #LPR "_r" #RPG "_u" #UNR "_nt" #NT, gemv_scalar<LPR, RPG, UNR, NT>, (64 / LPR) * RPG, false}
+#define VEC(LPR, RPG, UNR, NT, OPT)                                                             \
+    {"vec_l" #LPR "_r" #RPG "_u" #UNR "_nt" #NT "_o" #OPT, gemv_vec<LPR, RPG, UNR, NT, OPT>, \
+     (kBlock / 64) * (64 / LPR) * RPG, true, kBlock}
+#define SCL(LPR, RPG, UNR, NT)                                                              \
+    {"scl_l" #LPR "_r" #RPG "_u" #UNR "_nt" #NT, gemv_scalar<LPR, RPG, UNR, NT>,            \
+     (kBlock / 64) * (64 / LPR) * RPG, false, kBlock}
+#define RWB(NW, RPB, UNR)                                                                  \
+    {"rowblk_w" #NW "_r" #RPB "_u" #UNR, gemv_rowblock<NW, RPB, UNR, true>, RPB, true, NW * 64}
 
 static const Variant kVariants[] = {
     {"auto", nullptr, 0, false},   // 0
-    VEC(64, 4, 4, 0),          // 1
-    VEC(64, 4, 4, 1),           // 2
-    VEC(64, 2, 8, 0),          // 3
-    VEC(64, 2, 8, 1),           // 4
-    VEC(64, 8, 2, 1),           // 5
-    VEC(64, 1, 8, 1),           // 6
-    VEC(32, 2, 4, 1),           // 7
-    VEC(16, 2, 4, 1),           // 8
-    VEC(16, 4, 2, 1),           // 9
-    VEC(8, 2, 4, 1),            // 10
-    VEC(16, 1, 8, 1),           // 11
-    SCL(64, 4, 4, 1),           // 12
-    SCL(16, 2, 4, 1),           // 13
-    VEC(64, 4, 8, 1),           // 14
-    VEC(32, 4, 4, 1),           // 15
+    VEC(64, 4, 4, 0, 0),           // 1
+    VEC(64, 4, 4, 1, 0),           // 2
+    VEC(64, 2, 8, 1, 0),           // 3
+    VEC(64, 8, 2, 1, 0),           // 4
+    VEC(64, 1, 8, 1, 0),           // 5
+    VEC(32, 2, 4, 1, 0),           // 6
+    VEC(16, 2, 4, 1, 0),           // 7
+    VEC(8, 2, 4, 1, 0),            // 8
+    SCL(64, 4, 4, 1),              // 9
+    SCL(16, 2, 4, 1),              // 10
+    VEC(64, 4, 4, 1, 1),           // 11 pipelined
+    VEC(64, 2, 4, 1, 1),           // 12
+    VEC(64, 4, 4, 1, 2),           // 13 staggered
+    VEC(64, 2, 8, 1, 2),           // 14
+    VEC(64, 2, 4, 1, 3),           // 15 both
+    VEC(64, 4, 2, 1, 3),           // 16
+    VEC(32, 2, 4, 1, 2),           // 17
+    VEC(32, 2, 2, 1, 3),           // 18
+    VEC(64, 1, 4, 1, 1),           // 19
+    VEC(64, 1, 8, 1, 2),           // 20
+    RWB(4, 1, 4),                  // 21 row per workgroup
+    RWB(8, 1, 4),                  // 22
+    RWB(16, 1, 4),                 // 23
+    RWB(8, 2, 4),                  // 24
+    RWB(8, 1, 2),                  // 25
+    RWB(16, 1, 2),                 // 26
+    RWB(4, 2, 4),                  // 27
+    RWB(8, 2, 2),                  // 28
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
 // Shape-adaptive choice (see DESIGN.md §4 for the measurements behind it).
 static int pick_variant(int64_t lda, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
-    if (!vec) return K >= 256 ? 12 : 13;
-    if (K >= 2048) return 2;
-    if (K >= 768) return 7;
-    return 8;
+    if (!vec) return K >= 256 ? 9 : 10;
+    if (K > 1024) return 15;
+    return 19;
 }
 
 static int launch(int v, const double* A, int64_t lda, const double* x, double* y, int64_t M,
                   int64_t K, hipStream_t s) {
     const Variant& var = kVariants[v];
-    const int64_t waves = (M + var.rows_per_wave - 1) / var.rows_per_wave;
-    const int64_t blocks = (waves + (kBlock / 64) - 1) / (kBlock / 64);
+    const int64_t blocks = (M + var.rows_per_block - 1) / var.rows_per_block;
     if (blocks > 0x7fffffffLL) return fail(MVG_E_INVALID, "mvg_gemv: too many rows");
-    hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(kBlock), 0, s, A, lda, x, y, M, K);
+    hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(var.threads), 0, s, A, lda, x, y, M, K);
     MVG_HIP(hipGetLastError());
     return MVG_OK;
 }
@@ -246,24 +388,29 @@ __global__ __launch_bounds__(kBlock) void synth_fill_kernel(double* __restrict__
     }
 }
 
-// Read-only stream: HBM ceiling for a pure fp64 read with the same load shape as the GEMV.
+// Read-only stream: HBM ceiling for a pure fp64 read with the same load shape as the GEMV
+// (16 B per lane, nt, 8 loads in flight per lane). Each wave reads one contiguous segment.
 __global__ __launch_bounds__(kBlock) void stream_read_kernel(const double* __restrict__ src,
                                                              int64_t n2, double* sink) {
     constexpr int UNR = 8;
-    dbl2 acc = {0.0, 0.0};
-    const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t nthr = (int64_t)gridDim.x * kBlock;
     const dbl2* s = reinterpret_cast<const dbl2*>(src);
-    int64_t i = tid;
-    for (; i + (UNR - 1) * nthr < n2; i += UNR * nthr) {
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+    const int lane = threadIdx.x & 63;
+    const int64_t per = (n2 + nwaves - 1) / nwaves;
+    const int64_t b = wave * per;
+    const int64_t e = b + per < n2 ? b + per : n2;
+    dbl2 acc = {0.0, 0.0};
+    int64_t i = b + lane;
+    for (; i + 64 * (UNR - 1) < e; i += 64 * UNR) {
         dbl2 v[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(s + i + u * nthr);
+        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(s + i + 64 * u);
 #pragma unroll
         for (int u = 0; u < UNR; ++u) acc += v[u];
     }
-    for (; i < n2; i += nthr) acc += s[i];
-    if (acc.x == -1.0 && acc.y == -2.0) sink[tid] = acc.x;  // never true for real data; keeps loads live
+    for (; i < e; i += 64) acc += s[i];
+    if (acc.x == -1.0 && acc.y == -2.0) sink[threadIdx.x] = acc.x;  // never true for real data; keeps loads live
 }
 
 }  // namespace mvg
@@ -309,7 +456,7 @@ int mvg_gemv(const double* A, int64_t lda, const double* x, double* y, int64_t m
 int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {
     if (!src || !sink || n < 0 || (n & 1) || ((uintptr_t)src % 16))
         return fail(MVG_E_INVALID, "mvg_stream_read: need even n, 16-B aligned src, sink");
-    hipLaunchKernelGGL(stream_read_kernel, dim3(256 * 16), dim3(kBlock), 0, (hipStream_t)stream, src,
+    hipLaunchKernelGGL(stream_read_kernel, dim3(256 * 4), dim3(kBlock), 0, (hipStream_t)stream, src,
                        n / 2, sink);
     MVG_HIP(hipGetLastError());
     return MVG_OK;
