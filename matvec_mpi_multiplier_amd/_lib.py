@@ -135,7 +135,7 @@ def _load() -> C.CDLL:
             f"{LIB_PATH} is missing: the HIP library is required (no CPU fallback). "
             "Build it with `make -C <repo>` or `python -c 'import __graft_entry__ as g; g.build()'`."
         )
-    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(LIB_PATH)  # RTLD_LOCAL: a global RCCL ahead of torch's double-frees at exit
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
