@@ -199,7 +199,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
                 "traffic": traffic,
-                "kernel": "gemv_vec (auto variant), per GPU",
+                "kernel": kernel_name(sh) + ", per GPU",
                 "kernel_ms": round(kernel_ms, 5),
                 "bytes_per_launch": per_gpu,
                 "traffic_source": traffic_src,
@@ -237,6 +237,12 @@ def cpu_baseline(args, R, C, y_gpu):
                       f"(reference timing semantics: scatter from root + local sums + gather, max over ranks); "
                       f"GPU y matches to {rel:.1e}",
             "host_cpu": host_cpu()}
+
+
+def kernel_name(sh) -> str:
+    from matvec_mpi_multiplier_amd._lib import lib
+
+    return lib.mvg_gemv_variant_name(lib.mvg_gemv_auto_variant(sh.n_cols, sh.n_cols)).decode()
 
 
 def host_cpu():

@@ -143,11 +143,13 @@ int mvg_gemv(const double* d_A, int64_t lda, const double* d_x, double* d_y,
              int64_t m, int64_t k, void* stream);
 
 /* Same, with an explicit kernel variant (benchmarks / tests):
- *   0 = auto, 1 = wave-per-row x4 rows, 2 = 16-lane groups, 3 = scalar (no 16-B loads),
- *   4 = wave-per-row x2 rows, 5 = wave-per-row x8 rows, 6 = 8-lane groups ... */
+ *   0 = auto (shape-adaptive), 1.. = the table in csrc/gemv.hip (names via
+ *   mvg_gemv_variant_name: vec_* wave-owns-rows, rowblk_* row-per-workgroup, scl_* 8-B loads). */
 int mvg_gemv_variant(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                      int64_t m, int64_t k, int variant, void* stream);
 int mvg_gemv_variant_count(void);
+/* the variant mvg_gemv picks for a 16-B-aligned A, x with this lda and k */
+int mvg_gemv_auto_variant(int64_t lda, int64_t k);
 const char* mvg_gemv_variant_name(int variant);
 
 /* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */

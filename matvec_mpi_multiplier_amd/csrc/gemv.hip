@@ -349,14 +349,30 @@ static const Variant kVariants[] = {
     RWB(16, 1, 2),                 // 26
     RWB(4, 2, 4),                  // 27
     RWB(8, 2, 2),                  // 28
+    RWB(8, 4, 2),                  // 29
+    RWB(4, 4, 2),                  // 30
+    RWB(16, 2, 4),                 // 31
+    RWB(4, 2, 8),                  // 32
+    RWB(2, 2, 4),                  // 33
+    RWB(2, 4, 4),                  // 34
+    RWB(4, 4, 4),                  // 35
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
-// Shape-adaptive choice (see DESIGN.md §4 for the measurements behind it).
+// Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl):
+//   K >= 16384        row per workgroup, 4 waves x 2 rows, 8 x 16 B in flight per row per lane
+//   8192 <= K < 16384 row per workgroup, 8 waves x 2 rows (keeps >= 2 chunks per wave)
+//   1536 < K < 8192   wave-owns-2-rows, pipelined + staggered start column
+//   768 < K <= 1536   wave-owns-4-rows, pipelined
+//   K <= 768          one row per wave (the whole row is one chunk: 524288 short waves stream
+//                     consecutive memory, config 5's shard)
 static int pick_variant(int64_t lda, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) return K >= 256 ? 9 : 10;
-    if (K > 1024) return 15;
+    if (K >= 16384) return 32;
+    if (K >= 8192) return 24;
+    if (K > 1536) return 15;
+    if (K > 768) return 11;
     return 19;
 }
 
@@ -420,6 +436,8 @@ using namespace mvg;
 extern "C" {
 
 int mvg_gemv_variant_count(void) { return kNumVariants; }
+
+int mvg_gemv_auto_variant(int64_t lda, int64_t k) { return pick_variant(lda, k, true); }
 
 const char* mvg_gemv_variant_name(int v) {
     if (v < 0 || v >= kNumVariants) return "invalid";

@@ -1,9 +1,10 @@
+# One GPU round: parity tests, smoke, bench, rocprofv3 kernel stats, PMC passes.
 set -o pipefail
 mkdir -p gpurun_out
 echo "== pytest gpu"; timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 echo "== smoke"; timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-cat gpurun_out/smoke.log
+grep smoke gpurun_out/smoke.log
 echo "== bench"; timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 echo "== rocprof"; R=$PWD; cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-e2e > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof.err || { tail $R/gpurun_out/prof.err; exit 1; }
-find $R/gpurun_out/prof -name "*stats*" | head
+cd $R && bash tools/gpu_pmc.sh

@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--alg", required=True)
     ap.add_argument("--R", type=int, required=True)
     ap.add_argument("--C", type=int, required=True)
-    ap.add_argument("--kernel", default="gemv_vec")
+    ap.add_argument("--kernel", default="mvg::gemv_")
     ap.add_argument("--bytes-per-launch", type=int, default=None)
     args = ap.parse_args()
     counters = defaultdict(list)

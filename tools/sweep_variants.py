@@ -18,6 +18,10 @@ SHAPES = [
     ("cfg5_shard_524288x512", 524288, 512),
     ("cfg3_g8_strip_65536x8192", 65536, 8192),
     ("cfg4_block_65536x32768", 65536, 32768),
+    ("cfg3_g4_strip_65536x16384", 65536, 16384),
+    ("mid_1048576x2048", 1048576, 2048),
+    ("mid_524288x4096", 524288, 4096),
+    ("mid_2097152x1024", 2097152, 1024),
 ]
 
 
@@ -39,7 +43,7 @@ def main():
         ref = torch.mv(A, x)
         nbytes = 8 * (M * K + K + M)
         results = {}
-        variants = [v for v in range(nvar) if lib.mvg_gemv_variant_name(v).startswith(b"vec")] + [0]
+        variants = [v for v in range(nvar) if lib.mvg_gemv_variant_name(v).startswith((b"vec", b"rowblk"))] + [0]
         y = torch.empty(M, dtype=torch.float64, device=dev)
         for v in variants:
             y.zero_()
