@@ -63,17 +63,19 @@ int main(int argc, char** argv) {
         fprintf(stderr, "n_rows and n_cols must be >= 0\n");
         return 1;
     }
+    // G replaces mpiexec's P: $MVG_NGPUS, else every visible device (only then is the GPU
+    // runtime touched before the divisibility check, as MPI_Init precedes it in the reference)
+    int comm_sz = (int)env_long("MVG_NGPUS", 0);
     int ndev = 0;
-    int rc = mvg_device_count(&ndev);
-    if (rc != MVG_OK || ndev == 0) {
-        fprintf(stderr, "no GPU visible: %s\n", mvg_last_error());
-        return 1;
+    if (comm_sz <= 0) {
+        int rc0 = mvg_device_count(&ndev);
+        if (rc0 != MVG_OK || ndev == 0) {
+            fprintf(stderr, "no GPU visible: %s\n", mvg_last_error());
+            return 1;
+        }
+        comm_sz = ndev;
     }
-    const int comm_sz = (int)env_long("MVG_NGPUS", ndev);
-    if (comm_sz < 1 || comm_sz > ndev) {
-        fprintf(stderr, "MVG_NGPUS=%d but %d GPU(s) visible\n", comm_sz, ndev);
-        return 1;
-    }
+    int rc = MVG_OK;
     const long iters = std::max(1L, env_long("MVG_ITERS", 100));
     const char* data_dir = getenv("MVG_DATA_DIR") ? getenv("MVG_DATA_DIR") : "./data";
 
@@ -146,6 +148,10 @@ int main(int argc, char** argv) {
             printf("Unable to locate vector file '%s'\n", name);
             return 0;
         }
+    }
+    if ((rc = mvg_device_count(&ndev)) != MVG_OK || comm_sz > ndev) {
+        fprintf(stderr, "%d GPU(s) requested, %d visible: %s\n", comm_sz, ndev, mvg_last_error());
+        return 1;
     }
     // pinned host memory: distribution runs at full PCIe rate on every GPU's own link
     const bool pinned = nA > 0 && mvg_host_register(A.data(), nA * sizeof(double)) == MVG_OK;

@@ -1,0 +1,85 @@
+"""The drop-in executables bin/multiplier_{rowwise,colwise,blockwise}: the reference's process
+contract (argv, ./data inputs, messages, exit codes, ./data/out/<alg>.csv, y)."""
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DIR, REPO, max_rel
+
+ALGS = ("rowwise", "colwise", "blockwise")
+
+
+def run(alg, args, cwd, **env):
+    e = dict(os.environ, **{k: str(v) for k, v in env.items()})
+    return subprocess.run([os.path.join(REPO, "bin", f"multiplier_{alg}")] + [str(a) for a in args],
+                          cwd=cwd, env=e, capture_output=True, text=True, timeout=300)
+
+
+@pytest.fixture
+def workdir(tmp_path):
+    (tmp_path / "data" / "out").mkdir(parents=True)
+    for f in ("matrix_4_8.txt", "vector_8.txt"):
+        shutil.copy(os.path.join(GOLDEN_DIR, f), tmp_path / "data" / f)
+    return tmp_path
+
+
+def test_usage_without_arguments(workdir):
+    r = run("rowwise", [], workdir)
+    assert r.returncode == 1 and "usage" in r.stderr
+
+
+@pytest.mark.parametrize("alg,R,C,G,msg", [
+    ("rowwise", 4, 8, 3, "4 mod 3 = 1. Unable to parallellize task."),        # rowwise.c:72-75
+    ("colwise", 4, 8, 3, "8 mod 3 = 2. Unable to parallellize task."),        # colwise.c:151-154
+    ("blockwise", 5, 5, 2, "25 mod 2 = 1. Unable to parallellize task."),     # blockwise.c:277-281
+    ("blockwise", 3, 8, 4, "3 x 8 does not split over a 2 x 2 grid."),       # deliberate deviation
+])
+def test_indivisible_prints_error_and_exits_zero(workdir, alg, R, C, G, msg):
+    r = run(alg, [R, C], workdir, MVG_NGPUS=G)
+    assert r.returncode == 0
+    assert r.stdout.startswith("\nERROR!!!\n") and msg in r.stdout
+    assert not (workdir / "data" / "out" / f"{alg}.csv").exists()  # the check precedes the CSV
+
+
+def test_missing_input_file_message(workdir):
+    r = run("rowwise", [6, 6], workdir, MVG_NGPUS=1)
+    assert r.returncode == 0
+    assert "Reading matrix from file './data/matrix_6_6.txt'..." in r.stdout
+    assert "Unable to locate matrix file 'matrix_6_6.txt'" in r.stdout
+    # the CSV header is created before the load, as in rowwise.c:77-88
+    assert (workdir / "data" / "out" / "rowwise.csv").read_text() == "n_rows, n_cols, n_processes, time\n"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", ALGS)
+def test_fixture_run_matches_reference(workdir, golden, alg):
+    yout = workdir / "y.txt"
+    r = run(alg, [4, 8], workdir, MVG_NGPUS=1, MVG_ITERS=5, MVG_Y_OUT=yout)
+    assert r.returncode == 0, r.stderr
+    assert "n_rows = 4\nn_cols = 8\n" in r.stdout
+    assert "Reading vector from file './data/vector_8.txt'..." in r.stdout
+    y = np.loadtxt(yout)
+    assert max_rel(y, golden[f"fixture_4x8/{alg}/P1"]) <= 1e-12
+    lines = (workdir / "data" / "out" / f"{alg}.csv").read_text().splitlines()
+    assert lines[0] == "n_rows, n_cols, n_processes, time"
+    assert re.fullmatch(r"4, 8, 1, \d+\.\d{6}", lines[1]), lines[1]
+    # a second run appends a row (rowwise.c:163 opens with "a")
+    run(alg, [4, 8], workdir, MVG_NGPUS=1, MVG_ITERS=2)
+    assert len((workdir / "data" / "out" / f"{alg}.csv").read_text().splitlines()) == 3
+
+
+@pytest.mark.gpu
+def test_synthetic_large_run(workdir):
+    from oracle import oracle
+
+    R, C = 2048, 4096
+    yout = workdir / "y.txt"
+    r = run("colwise", [R, C], workdir, MVG_NGPUS=1, MVG_ITERS=3, MVG_SYNTH=1, MVG_Y_OUT=yout)
+    assert r.returncode == 0, r.stderr
+    assert "device-resident" in r.stdout
+    y = np.loadtxt(yout)
+    assert max_rel(y, oracle.multiply("colwise", oracle.synth(R, C, 42), oracle.synth(1, C, 4242)[0], 1)) <= 1e-12
