@@ -135,34 +135,7 @@ def main():
     # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
     e2e = None
     if not args.no_e2e and args.e2e_iters > 0:
-        A = x = None
-        if rank == 0:
-            A = mm.synth_host(R, C, 42)
-            x = mm.synth_host(1, C, 4242)[0]
-            from matvec_mpi_multiplier_amd._lib import lib as _l
-
-            _l.mvg_host_register(A.ctypes.data, A.nbytes)
-        times = []
-        for _ in range(args.e2e_iters):
-            barrier()
-            ts = time.perf_counter()
-            eng.distribute(A, x)
-            eng.multiply()
-            y2 = eng.collect()
-            barrier()
-            tt = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=f"cuda:{local}")
-            if distributed:
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            times.append(float(tt[0]))
-        if rank == 0:
-            assert np.array_equal(y2, y), "end-to-end y differs from device-resident y"
-            from matvec_mpi_multiplier_amd._lib import lib as _l
-
-            _l.mvg_host_unregister(A.ctypes.data)
-        e2e = {"mean_s": float(np.mean(times)), "iters": len(times),
-               "GBps": total_bytes / float(np.mean(times)) / 1e9,
-               "semantics": "reference (root holds A, x in host memory; distribute + multiply + y on root)",
-               "distribution": "per-GPU H2D" if not distributed else "root H2D + ncclSend over xGMI"}
+        e2e = end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y, total_bytes, local)
 
     # ---- CPU baseline: rank 0 at N = 1 only
     cpu = None
@@ -213,6 +186,94 @@ def main():
     comm.destroy()
     if distributed:
         dist.destroy_process_group()
+
+
+def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_bytes, local):
+    """The reference's timing semantics on the GPU path: A and x preloaded in the root's host
+    memory; each iteration distributes them, multiplies, and ends when the root holds y (max over
+    ranks). Two distributions:
+      shared    : the root's A lives in host shared memory every rank maps; each GPU pulls its own
+                  shard over its own PCIe link, all at once (MPICH's shared-memory scatter analog;
+                  N = 1: one process, plain pinned memory).
+      root_send : only the root touches A; it stages each peer's shard through its GPU and
+                  ncclSends it over xGMI (the reference's sequential root sends). N > 1 only."""
+    import torch
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd._lib import lib as _l
+
+    def timed(fn):
+        times = []
+        for _ in range(args.e2e_iters):
+            barrier()
+            ts = time.perf_counter()
+            y = fn()
+            barrier()
+            tt = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=f"cuda:{local}")
+            if distributed:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            times.append(float(tt[0]))
+        if rank == 0:
+            assert np.array_equal(y, y_ref), "end-to-end y differs from the device-resident y"
+        return {"mean_s": float(np.mean(times)), "iters": len(times),
+                "GBps": total_bytes / float(np.mean(times)) / 1e9}
+
+    out = {"semantics": "reference: root holds A, x in host memory; distribute + multiply + y on root"}
+    nbytes = R * C * 8
+    shm = None
+    if not distributed:
+        A = mm.synth_host(R, C, 42)
+    else:
+        A = None
+        from multiprocessing import resource_tracker, shared_memory
+
+        name = f"mvg_bench_{os.environ.get('MASTER_PORT', '0')}"
+        free = 0
+        try:
+            st = os.statvfs("/dev/shm")
+            free = st.f_bavail * st.f_frsize
+        except OSError:
+            pass
+        ok = torch.tensor([1 if free > nbytes + (1 << 30) else 0], device=f"cuda:{local}")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok[0]):
+            if rank == 0:
+                shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
+                A = np.ndarray((R, C), dtype=np.float64, buffer=shm.buf)
+                _l.mvg_synth_fill_host(A.ctypes.data, C, R, C, 0, 0, C, 42)
+            barrier()
+            if rank != 0:
+                shm = shared_memory.SharedMemory(name=name)
+                resource_tracker.unregister(shm._name, "shared_memory")
+                A = np.ndarray((R, C), dtype=np.float64, buffer=shm.buf)
+        else:
+            out["shared"] = f"skipped: /dev/shm has {free >> 30} GiB free, needs {nbytes >> 30} GiB"
+    x = mm.synth_host(1, C, 4242)[0]
+    have_shared = A is not None
+    if distributed and not have_shared and rank == 0:
+        A = mm.synth_host(R, C, 42)  # root-only copy for the root_send distribution
+    pinned = A is not None and _l.mvg_host_register(A.ctypes.data, A.nbytes) == 0
+    if have_shared:
+        out["shared"] = timed(lambda: (eng.distribute_shared(A, x), eng.multiply(), eng.collect())[2])
+        out["shared"]["distribution"] = ("per-GPU H2D from " + ("shared " if distributed else "")
+                                         + ("pinned" if pinned else "pageable") + " host memory")
+    if distributed:
+        out["root_send"] = timed(lambda: (eng.distribute(A if rank == 0 else None, x), eng.multiply(),
+                                          eng.collect())[2])
+        out["root_send"]["distribution"] = "root H2D staging + ncclSend over xGMI"
+    if pinned:
+        _l.mvg_host_unregister(A.ctypes.data)
+    if shm is not None:
+        barrier()
+        eng._keep = None
+        del A
+        try:
+            shm.close()
+        except BufferError:
+            pass
+        if rank == 0:
+            shm.unlink()
+    return out
 
 
 def cpu_baseline(args, R, C, y_gpu):

@@ -186,6 +186,11 @@ typedef struct mvg_engine mvg_engine;
 int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm* comm);
 int mvg_engine_shard(const mvg_engine* e, int local_index, mvg_shard* out);
 int mvg_engine_distribute(mvg_engine* e, const double* A_host, const double* x_host);
+/* One process per GPU on one node: the root's A, x live in host memory every rank maps
+ * (shared memory); each GPU pulls its own shard over its own PCIe link, all in parallel (the
+ * analog of MPICH's shared-memory MPI_Scatter on one host). Every rank passes the full A, x.
+ * In single-process mode identical to mvg_engine_distribute. */
+int mvg_engine_distribute_shared(mvg_engine* e, const double* A_shared, const double* x_shared);
 int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x);
 int mvg_engine_multiply(mvg_engine* e);
 int mvg_engine_sync(mvg_engine* e);

@@ -113,6 +113,7 @@ SIGNATURES = {
     "mvg_engine_create": (C.c_int, [C.POINTER(_p), C.c_int, _i64, _i64, _p]),
     "mvg_engine_shard": (C.c_int, [_p, C.c_int, C.POINTER(Shard)]),
     "mvg_engine_distribute": (C.c_int, [_p, _p, _p]),
+    "mvg_engine_distribute_shared": (C.c_int, [_p, _p, _p]),
     "mvg_engine_fill_synth": (C.c_int, [_p, C.c_uint64, C.c_uint64]),
     "mvg_engine_multiply": (C.c_int, [_p]),
     "mvg_engine_sync": (C.c_int, [_p]),

@@ -157,6 +157,21 @@ int h2d_region(double* dst, const double* host, int64_t ld_host, int64_t rows, i
 inline int64_t x_off(const mvg_shard& p) { return p.col_off; }
 inline int64_t x_len(const mvg_shard& p) { return p.n_cols; }
 
+// Every local device pulls its own shard (and x segment) from host memory that holds the
+// whole A and x, over its own PCIe link, concurrently (one stream per device).
+int distribute_direct(mvg_engine* e, const double* A, const double* x) {
+    const int64_t C = e->C;
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        const mvg_shard& p = s.plan;
+        int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
+        if (rc != MVG_OK) return rc;
+        rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
+        if (rc != MVG_OK) return rc;
+    }
+    return MVG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -361,14 +376,8 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
     if (root && (!x || (!A && e->R * C > 0))) return fail(MVG_E_INVALID, "root needs A and x");
 
     if (e->single_process) {
-        for (auto& s : e->shards) {
-            MVG_HIP(hipSetDevice(s.device));
-            const mvg_shard& p = s.plan;
-            int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
-            if (rc != MVG_OK) return rc;
-            rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
-            if (rc != MVG_OK) return rc;
-        }
+        int rc = distribute_direct(e, A, x);
+        if (rc != MVG_OK) return rc;
     } else {
         // exactly one local shard
         Shard& s = e->shards[0];
@@ -440,6 +449,16 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
             }
         }
     }
+    e->distributed = true;
+    return MVG_OK;
+}
+
+int mvg_engine_distribute_shared(mvg_engine* e, const double* A, const double* x) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    if (!x || (!A && e->R * e->C > 0)) return fail(MVG_E_INVALID, "every rank needs the shared A and x");
+    DeviceGuard g;
+    int rc = distribute_direct(e, A, x);
+    if (rc != MVG_OK) return rc;
     e->distributed = true;
     return MVG_OK;
 }

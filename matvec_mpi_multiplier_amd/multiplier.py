@@ -263,6 +263,15 @@ class Multiplier:
         self._keep = (A, x)
         check(lib.mvg_engine_distribute(self.handle, pa, px), "mvg_engine_distribute")
 
+    def distribute_shared(self, A: np.ndarray, x: np.ndarray) -> None:
+        """Every rank passes the root's A, x mapped from shared host memory; each GPU pulls its
+        own shard over its own PCIe link, concurrently."""
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        self._keep = (A, x)
+        check(lib.mvg_engine_distribute_shared(self.handle, A.ctypes.data, x.ctypes.data),
+              "mvg_engine_distribute_shared")
+
     def fill_synth(self, seed_a: int = SEED_A, seed_x: int = SEED_X) -> None:
         check(lib.mvg_engine_fill_synth(self.handle, seed_a, seed_x), "mvg_engine_fill_synth")
 

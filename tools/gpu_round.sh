@@ -1,6 +1,7 @@
 # One GPU round: parity tests, smoke, bench, rocprofv3 kernel stats, PMC passes.
 set -o pipefail
 mkdir -p gpurun_out
+df -h /dev/shm /tmp 2>/dev/null | tail -2; free -g | head -2; nproc
 echo "== pytest gpu"; timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 echo "== smoke"; timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 grep smoke gpurun_out/smoke.log
