@@ -356,6 +356,11 @@ static const Variant kVariants[] = {
     RWB(2, 2, 4),                  // 33
     RWB(2, 4, 4),                  // 34
     RWB(4, 4, 4),                  // 35
+    VEC(64, 2, 4, 1, 0),           // 36 short rows: 2 rows per wave, unpipelined
+    VEC(32, 1, 4, 1, 1),           // 37 two 512-col rows per wave, pipelined
+    VEC(32, 2, 4, 1, 1),           // 38
+    VEC(64, 1, 2, 1, 1),           // 39
+    VEC(16, 1, 4, 1, 0),           // 40
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 

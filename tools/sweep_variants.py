@@ -22,20 +22,25 @@ SHAPES = [
     ("mid_1048576x2048", 1048576, 2048),
     ("mid_524288x4096", 524288, 4096),
     ("mid_2097152x1024", 2097152, 1024),
+    ("cfg5_full_4194304x512", 4194304, 512),
+    ("cfg4_full_131072sq", 131072, 131072),
 ]
 
 
 def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
-    max_elems = max(m * k for _, m, k in SHAPES)
+    max_elems = max(m * k for n, m, k in SHAPES if not only or n in only)
     buf = torch.empty(max_elems, dtype=torch.float64, device=dev)
     xbuf = torch.empty(65536, dtype=torch.float64, device=dev)
     sink = torch.zeros(256 * 16 * 256, dtype=torch.float64, device=dev)
     nvar = lib.mvg_gemv_variant_count()
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     iters = 10
     for name, M, K in SHAPES:
+        if only and name not in only:
+            continue
         A = buf[: M * K].view(M, K)
         x = xbuf[:K]
         check(lib.mvg_synth_fill_device(A.data_ptr(), K, M, K, 0, 0, K, 42, s), "fill A")
