@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
     ap.add_argument("--cols", type=int, default=SHARD)
     ap.add_argument("--e2e-iters", type=int, default=3)
+    ap.add_argument("--event-every", type=int, default=5,
+                    help="bracket every Nth step's GEMV with HIP events (kernel duration for the roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=None)
@@ -72,6 +74,11 @@ def pmc_traffic(alg: str, R: int, C: int, n: int):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line (rank 0): anything the runtimes print on fd 1
+    # (RCCL's init banner, HIP messages) is sent to stderr instead.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -105,7 +112,7 @@ def main():
         eng.multiply()
     eng.sync()
 
-    eng.kernel_timing(True)
+    eng.kernel_timing(args.event_every)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -114,7 +121,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kt = eng.kernel_ms()
-    eng.kernel_timing(False)
+    eng.kernel_timing(0)
 
     t = torch.tensor([elapsed, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
     if distributed:
@@ -182,7 +189,8 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
         }
-        print(json.dumps(out), flush=True)
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
 
     eng.destroy()
     comm.destroy()

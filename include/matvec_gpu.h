@@ -198,8 +198,9 @@ int mvg_engine_collect(mvg_engine* e, double* y_host);
 /* per-local-device stream (hipStream_t as void*), e.g. for hipEvent timing by the caller */
 int mvg_engine_stream(const mvg_engine* e, int local_index, void** stream);
 /* Average GEMV kernel time (ms) over the multiply calls since the last reset, measured with
- * hipEvents bracketing the kernel on each local device's stream (max over local devices). */
-int mvg_engine_kernel_timing(mvg_engine* e, int enable);
+ * hipEvents bracketing the kernel on each local device's stream (max over local devices).
+ * every = N > 0 brackets every Nth multiply call (1 = all); 0 turns timing off. */
+int mvg_engine_kernel_timing(mvg_engine* e, int every);
 int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches);
 int mvg_engine_destroy(mvg_engine* e);
 

@@ -93,7 +93,8 @@ struct mvg_engine {
     bool single_process = false;  // all ranks in this process
     bool always_collect = false;  // run the collectives even at nranks == 1 (tests)
     bool distributed = false;
-    bool timing = false;
+    int timing_every = 0;       // record kernel events on every Nth multiply (0 = off)
+    int64_t multiply_calls = 0;
     double kernel_ms_sum = 0.0;
     int64_t kernel_launches = 0;
     std::vector<Shard> shards;
@@ -467,7 +468,8 @@ int mvg_engine_kernel_timing(mvg_engine* e, int enable) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
     int rc = mvg_engine_sync(e);
     if (rc != MVG_OK) return rc;
-    e->timing = enable != 0;
+    e->timing_every = enable > 0 ? enable : 0;
+    e->multiply_calls = 0;
     e->kernel_ms_sum = 0.0;
     e->kernel_launches = 0;
     return MVG_OK;
@@ -479,13 +481,14 @@ int mvg_engine_multiply(mvg_engine* e) {
     DeviceGuard g;
     const int nsteps = e->shards[0].nsteps;
     const bool solo = nsteps == 0;  // P == 1: the product goes straight into y
+    const bool timed = e->timing_every > 0 && (e->multiply_calls++ % e->timing_every) == 0;
     // 1) local product on every device
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
         const mvg_shard& p = s.plan;
         double* out = solo ? s.dy : s.dy_part;
         hipEvent_t t0 = nullptr, t1 = nullptr;
-        if (e->timing) {
+        if (timed) {
             if (s.ev_used == s.ev_pool.size()) {
                 hipEvent_t a, b;
                 MVG_HIP(hipEventCreate(&a));
@@ -499,7 +502,7 @@ int mvg_engine_multiply(mvg_engine* e) {
         }
         int rc = mvg_gemv(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream);
         if (rc != MVG_OK) return rc;
-        if (e->timing) MVG_HIP(hipEventRecord(t1, s.stream));
+        if (timed) MVG_HIP(hipEventRecord(t1, s.stream));
     }
     // 2) the exchange step, from the shared schedule (mvg_plan_exchange)
     for (int k = 0; k < nsteps; ++k) {
@@ -531,8 +534,8 @@ int mvg_engine_sync(mvg_engine* e) {
         MVG_HIP(hipStreamSynchronize(s.copy_stream));
         MVG_HIP(hipStreamSynchronize(s.stream));
     }
-    if (e->timing) {
-        // per multiply call: max over local devices, then summed
+    if (e->timing_every > 0) {
+        // per timed multiply call: max over local devices, then summed
         size_t n = e->shards.empty() ? 0 : e->shards[0].ev_used;
         for (size_t k = 0; k < n; ++k) {
             float worst = 0.f;

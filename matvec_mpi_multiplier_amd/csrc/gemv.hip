@@ -381,13 +381,20 @@ static int pick_variant(int64_t lda, int64_t K, bool aligned) {
     return 19;
 }
 
+// HIP caps a launch at gridDim.x * blockDim.x < 2^32 threads: very tall problems run as
+// several launches over consecutive row ranges (each range is an independent GEMV).
 static int launch(int v, const double* A, int64_t lda, const double* x, double* y, int64_t M,
                   int64_t K, hipStream_t s) {
     const Variant& var = kVariants[v];
-    const int64_t blocks = (M + var.rows_per_block - 1) / var.rows_per_block;
-    if (blocks > 0x7fffffffLL) return fail(MVG_E_INVALID, "mvg_gemv: too many rows");
-    hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(var.threads), 0, s, A, lda, x, y, M, K);
-    MVG_HIP(hipGetLastError());
+    const int64_t max_blocks = (1ll << 31) / var.threads;
+    const int64_t max_rows = max_blocks * var.rows_per_block;
+    for (int64_t r0 = 0; r0 < M; r0 += max_rows) {
+        const int64_t m = M - r0 < max_rows ? M - r0 : max_rows;
+        const int64_t blocks = (m + var.rows_per_block - 1) / var.rows_per_block;
+        hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(var.threads), 0, s, A + r0 * lda, lda, x,
+                           y + r0, m, K);
+        MVG_HIP(hipGetLastError());
+    }
     return MVG_OK;
 }
 

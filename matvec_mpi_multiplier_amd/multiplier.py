@@ -290,8 +290,9 @@ class Multiplier:
         check(lib.mvg_engine_collect(self.handle, y.ctypes.data), "mvg_engine_collect")
         return y[: self.R]
 
-    def kernel_timing(self, enable: bool) -> None:
-        check(lib.mvg_engine_kernel_timing(self.handle, int(enable)), "mvg_engine_kernel_timing")
+    def kernel_timing(self, every: int) -> None:
+        """Bracket every `every`-th multiply's GEMV with HIP events (0 = off)."""
+        check(lib.mvg_engine_kernel_timing(self.handle, int(every)), "mvg_engine_kernel_timing")
 
     def kernel_ms(self) -> KernelTiming:
         ms, n = C.c_double(), C.c_int64()

@@ -28,6 +28,7 @@ SHAPES = [
 
 
 def main():
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     max_elems = max(m * k for n, m, k in SHAPES if not only or n in only)
@@ -36,7 +37,6 @@ def main():
     sink = torch.zeros(256 * 16 * 256, dtype=torch.float64, device=dev)
     nvar = lib.mvg_gemv_variant_count()
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     iters = 10
     for name, M, K in SHAPES:
         if only and name not in only:
