@@ -333,7 +333,7 @@ def _splits(alg, R, C, p):
 def kernel_name(sh) -> str:
     from matvec_mpi_multiplier_amd._lib import lib
 
-    return lib.mvg_gemv_variant_name(lib.mvg_gemv_auto_variant(sh.n_cols, sh.n_cols)).decode()
+    return lib.mvg_gemv_variant_name(lib.mvg_gemv_auto_variant(sh.n_cols, sh.n_rows, sh.n_cols)).decode()
 
 
 def host_cpu():

@@ -148,8 +148,8 @@ int mvg_gemv(const double* d_A, int64_t lda, const double* d_x, double* d_y,
 int mvg_gemv_variant(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                      int64_t m, int64_t k, int variant, void* stream);
 int mvg_gemv_variant_count(void);
-/* the variant mvg_gemv picks for a 16-B-aligned A, x with this lda and k */
-int mvg_gemv_auto_variant(int64_t lda, int64_t k);
+/* the variant mvg_gemv picks for a 16-B-aligned A, x with this lda, m and k */
+int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k);
 const char* mvg_gemv_variant_name(int variant);
 
 /* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */

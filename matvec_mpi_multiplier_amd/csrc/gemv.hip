@@ -173,7 +173,16 @@ __global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A,
 // instead of thousands of scattered row positions. Per-wave partial sums meet in LDS and are
 // added in wave order (fixed, deterministic). Pipelined: chunk i+NW's loads issue before
 // chunk i's FMAs.
-template <int NW, int RPB, int UNR, bool NT>
+// XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so without a
+// remap XCD k streams rows {b : b % 8 == k}; with it, XCD k streams one contiguous row range.
+// Bijective for any grid size (the guide's remap for nwg % 8 != 0). Speed only, never
+// correctness.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
+    const int64_t q = nwg / 8, r = nwg % 8, xcd = b % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+template <int NW, int RPB, int UNR, bool NT, bool XCD = false>
 __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
                                                          const double* __restrict__ x,
                                                          double* __restrict__ y, int64_t M,
@@ -181,7 +190,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restric
     __shared__ double part[NW][RPB];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t row0 = (int64_t)blockIdx.x * RPB;
+    const int64_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t row0 = bid * RPB;
     const double* arow[RPB];
 #pragma unroll
     for (int r = 0; r < RPB; ++r) {
@@ -318,6 +328,8 @@ struct Variant {
      (kBlock / 64) * (64 / LPR) * RPG, false, kBlock}
 #define RWB(NW, RPB, UNR)                                                                  \
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR, gemv_rowblock<NW, RPB, UNR, true>, RPB, true, NW * 64}
+#define RWX(NW, RPB, UNR)                                                                  \
+    {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xcd", gemv_rowblock<NW, RPB, UNR, true, true>, RPB, true, NW * 64}
 
 static const Variant kVariants[] = {
     {"auto", nullptr, 0, false},   // 0
@@ -361,21 +373,28 @@ static const Variant kVariants[] = {
     VEC(32, 2, 4, 1, 1),           // 38
     VEC(64, 1, 2, 1, 1),           // 39
     VEC(16, 1, 4, 1, 0),           // 40
+    RWX(4, 2, 8),                  // 41 XCD-remapped
+    RWX(8, 2, 4),                  // 42
+    RWB(8, 2, 8),                  // 43
+    RWB(4, 3, 8),                  // 44
+    RWX(4, 1, 8),                  // 45
+    RWB(4, 1, 8),                  // 46
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
 // Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl):
-//   K >= 16384        row per workgroup, 4 waves x 2 rows, 8 x 16 B in flight per row per lane
-//   8192 <= K < 16384 row per workgroup, 8 waves x 2 rows (keeps >= 2 chunks per wave)
+//   K >= 16384        row per workgroup, 4 waves x 2 rows, 8 x 16 B in flight per row per lane;
+//                     XCD-contiguous row ranges once there are >= 16384 workgroups (+0.3-0.8 %)
+//   8192 <= K < 16384 row per workgroup, 8 waves x 2 rows, XCD-contiguous (>= 2 chunks per wave)
 //   1536 < K < 8192   wave-owns-2-rows, pipelined + staggered start column
 //   768 < K <= 1536   wave-owns-4-rows, pipelined
 //   K <= 768          one row per wave (the whole row is one chunk: 524288 short waves stream
 //                     consecutive memory, config 5's shard)
-static int pick_variant(int64_t lda, int64_t K, bool aligned) {
+static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) return K >= 256 ? 9 : 10;
-    if (K >= 16384) return 32;
-    if (K >= 8192) return 24;
+    if (K >= 16384) return M >= 32768 ? 41 : 32;
+    if (K >= 8192) return 42;
     if (K > 1536) return 15;
     if (K > 768) return 11;
     return 19;
@@ -449,7 +468,7 @@ extern "C" {
 
 int mvg_gemv_variant_count(void) { return kNumVariants; }
 
-int mvg_gemv_auto_variant(int64_t lda, int64_t k) { return pick_variant(lda, k, true); }
+int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k) { return pick_variant(lda, m, k, true); }
 
 const char* mvg_gemv_variant_name(int v) {
     if (v < 0 || v >= kNumVariants) return "invalid";
@@ -472,7 +491,7 @@ int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, i
     if (!A || !x) return fail(MVG_E_INVALID, "mvg_gemv: null A or x");
     if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv: lda < k");
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
-    int v = variant == 0 ? pick_variant(lda, k, aligned) : variant;
+    int v = variant == 0 ? pick_variant(lda, m, k, aligned) : variant;
     if (kVariants[v].vec && !(aligned && lda % 2 == 0))
         return fail(MVG_E_INVALID, "mvg_gemv: 16-B variant needs even lda and 16-B aligned A, x");
     return launch(v, A, lda, x, y, m, k, s);
