@@ -240,3 +240,32 @@ def test_text_input_end_to_end(tmp_path, comm1):
             e.distribute(A, x)
             e.multiply()
             assert max_rel(e.collect(), oracle.multiply(alg, A, x, 1)) <= TOL
+
+
+def test_engine_distribute_shared_and_kernel_timing(comm1, golden):
+    A, x = oracle.synth(480, 480, 42), oracle.synth(1, 480, 4242)[0]
+    for alg in ("rowwise", "colwise", "blockwise"):
+        with mm.Multiplier(alg, 480, 480, comm1) as e:
+            e.distribute_shared(A, x)
+            e.kernel_timing(2)
+            for _ in range(6):
+                e.multiply()
+            kt = e.kernel_ms()
+            e.kernel_timing(0)
+            assert kt.launches == 3 and kt.avg_ms > 0
+            assert max_rel(e.collect(), golden[f"sq_480/{alg}/P1"]) <= TOL
+
+
+def test_engine_multiply_before_inputs_is_state_error(comm1):
+    with mm.Multiplier("rowwise", 8, 8, comm1) as e:
+        with pytest.raises(_lib.MvgError) as err:
+            e.multiply()
+        assert err.value.code == _lib.MVG_E_STATE
+
+
+def test_auto_variant_names_match_the_dispatch_table():
+    names = {k: _lib.lib.mvg_gemv_variant_name(_lib.lib.mvg_gemv_auto_variant(k, m, k)).decode()
+             for m, k in ((16384, 16384), (65536, 32768), (65536, 8192), (524288, 4096), (2097152, 1024),
+                          (4194304, 512))}
+    assert names[16384] == "rowblk_w4_r2_u8" and names[32768] == "rowblk_w4_r2_u8_xcd"
+    assert names[8192] == "rowblk_w8_r2_u4_xcd" and names[512] == "vec_l64_r1_u4_nt1_o1"
