@@ -18,7 +18,9 @@
 // variant (8 B per lane, still coalesced) covers it.
 #include "common.h"
 
+#include <map>
 #include <mutex>
+#include <utility>
 
 namespace mvg {
 
@@ -182,16 +184,15 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-template <int NW, int RPB, int UNR, bool NT, bool XCD = false>
-__global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
-                                                         const double* __restrict__ x,
-                                                         double* __restrict__ y, int64_t M,
-                                                         int64_t K) {
-    __shared__ double part[NW][RPB];
+// The workgroup's work: rows [row0, +RPB) over columns [0, K) of A/x (callers offset A and x
+// for a K-range); writes the row sums to out[r * out_stride].
+template <int NW, int RPB, int UNR, bool NT>
+__device__ __forceinline__ void rowblock_body(const double* __restrict__ A, int64_t lda,
+                                              const double* __restrict__ x, int64_t M, int64_t K,
+                                              int64_t row0, double* __restrict__ out,
+                                              int64_t out_stride, double (&part)[NW][RPB]) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-    const int64_t row0 = bid * RPB;
     const double* arow[RPB];
 #pragma unroll
     for (int r = 0; r < RPB; ++r) {
@@ -252,7 +253,50 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restric
         double s = 0.0;
 #pragma unroll
         for (int v = 0; v < NW; ++v) s += part[v][threadIdx.x];
-        y[row0 + threadIdx.x] = s;
+        out[threadIdx.x * out_stride] = s;
+    }
+}
+
+template <int NW, int RPB, int UNR, bool NT, bool XCD = false>
+__global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
+                                                         const double* __restrict__ x,
+                                                         double* __restrict__ y, int64_t M,
+                                                         int64_t K) {
+    __shared__ double part[NW][RPB];
+    const int64_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t row0 = bid * RPB;
+    rowblock_body<NW, RPB, UNR, NT>(A, lda, x, M, K, row0, y + row0, 1, part);
+}
+
+// Split-K for short, wide problems (few rows, so too few row workgroups to fill 256 CUs):
+// workgroup b takes row block b / S and K-range b % S of width ks (a multiple of the chunk), so
+// consecutive workgroups still read consecutive memory; the partial sums go to
+// partial[row * S + s] and gemv_splitk_reduce adds them in s order (deterministic).
+template <int NW, int RPB, int UNR, bool NT>
+__global__ __launch_bounds__(NW * 64) void gemv_rowblock_split(const double* __restrict__ A,
+                                                               int64_t lda,
+                                                               const double* __restrict__ x,
+                                                               double* __restrict__ partial,
+                                                               int64_t M, int64_t K, int64_t ks,
+                                                               int64_t S) {
+    __shared__ double part[NW][RPB];
+    const int64_t rb = (int64_t)blockIdx.x / S;
+    const int64_t sp = (int64_t)blockIdx.x % S;
+    const int64_t k0 = sp * ks;
+    const int64_t k1 = k0 + ks < K ? k0 + ks : K;
+    const int64_t row0 = rb * RPB;
+    rowblock_body<NW, RPB, UNR, NT>(A + k0, lda, x + k0, M, k1 > k0 ? k1 - k0 : 0, row0,
+                                    partial + row0 * S + sp, S, part);
+}
+
+__global__ void gemv_splitk_reduce(const double* __restrict__ partial, int64_t S,
+                                   double* __restrict__ y, int64_t M) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < M;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const double* p = partial + r * S;
+        double s = 0.0;
+        for (int64_t j = 0; j < S; ++j) s += p[j];
+        y[r] = s;
     }
 }
 
@@ -312,12 +356,17 @@ __global__ __launch_bounds__(kBlock) void gemv_scalar(const double* __restrict__
 // ------------------------------------------------------------------ variant table
 typedef void (*gemv_fn)(const double*, int64_t, const double*, double*, int64_t, int64_t);
 
+typedef void (*gemv_split_fn)(const double*, int64_t, const double*, double*, int64_t, int64_t,
+                              int64_t, int64_t);
+
 struct Variant {
     const char* name;
     gemv_fn fn;
     int rows_per_block;  // rows one workgroup covers
     bool vec;            // needs 16-B alignment + even lda
     int threads;         // workgroup size
+    gemv_split_fn split = nullptr;  // split-K form (row-per-workgroup variants only)
+    int chunk = 0;                  // columns per wave chunk (split width granule)
 };
 
 #define VEC(LPR, RPG, UNR, NT, OPT)                                                             \
@@ -328,6 +377,9 @@ struct Variant {
      (kBlock / 64) * (64 / LPR) * RPG, false, kBlock}
 #define RWB(NW, RPB, UNR)                                                                  \
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR, gemv_rowblock<NW, RPB, UNR, true>, RPB, true, NW * 64}
+#define RWS(NW, RPB, UNR)                                                                  \
+    {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_splitk", nullptr, RPB, true, NW * 64,                \
+     gemv_rowblock_split<NW, RPB, UNR, true>, 128 * UNR}
 #define RWX(NW, RPB, UNR)                                                                  \
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xcd", gemv_rowblock<NW, RPB, UNR, true, true>, RPB, true, NW * 64}
 
@@ -379,10 +431,18 @@ static const Variant kVariants[] = {
     RWB(4, 3, 8),                  // 44
     RWX(4, 1, 8),                  // 45
     RWB(4, 1, 8),                  // 46
+    RWS(4, 2, 8),                  // 47 split-K
+    RWS(4, 2, 4),                  // 48
+    RWS(4, 1, 8),                  // 49
+    RWS(8, 1, 4),                  // 50
+    RWS(4, 1, 4),                  // 51
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
+constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4 per CU)
+
 // Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl):
+//   K >= 8192, fewer than 512 row workgroups: the same, split-K (deterministic two-pass)
 //   K >= 16384        row per workgroup, 4 waves x 2 rows, 8 x 16 B in flight per row per lane;
 //                     XCD-contiguous row ranges once there are >= 16384 workgroups (+0.3-0.8 %)
 //   8192 <= K < 16384 row per workgroup, 8 waves x 2 rows, XCD-contiguous (>= 2 chunks per wave)
@@ -393,19 +453,72 @@ constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) return K >= 256 ? 9 : 10;
-    if (K >= 16384) return M >= 32768 ? 41 : 32;
-    if (K >= 8192) return 42;
+    if (K >= 8192) {
+        // short, wide (the reference's 120..1200 x 60000 set): too few row workgroups -> split-K
+        if ((M + 1) / 2 < kSplitTarget / 2) return K >= 16384 ? 47 : 48;
+        if (K >= 16384) return M >= 32768 ? 41 : 32;
+        return 42;
+    }
     if (K > 1536) return 15;
     if (K > 768) return 11;
     return 19;
 }
 
+// Split-K workspace: one fp64 buffer per (device, stream), grown on demand (growth frees the
+// old buffer, which hipFree synchronises); a split launch is not graph-capturable on first use.
+static std::mutex g_ws_mu;
+static std::map<std::pair<int, hipStream_t>, std::pair<double*, size_t>> g_ws;
+
+static int workspace(hipStream_t s, size_t n, double** out) {
+    int dev = 0;
+    MVG_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto& e = g_ws[{dev, s}];
+    if (e.second < n) {
+        if (e.first) MVG_HIP(hipFree(e.first));
+        e = {nullptr, 0};
+        MVG_HIP(hipMalloc((void**)&e.first, n * sizeof(double)));
+        e.second = n;
+    }
+    *out = e.first;
+    return MVG_OK;
+}
+
+// Number of K-ranges for a split launch: enough workgroups to fill the chip, each wave keeping
+// at least one whole chunk; `force` keeps >= 2 whenever K allows (explicit split variants).
+static int64_t split_count(const Variant& var, int64_t M, int64_t K, bool force) {
+    const int64_t nrb = (M + var.rows_per_block - 1) / var.rows_per_block;
+    const int64_t nw = var.threads / 64;
+    int64_t smax = K / (nw * var.chunk);
+    if (smax < 1) smax = 1;
+    int64_t S = (kSplitTarget + nrb - 1) / nrb;
+    if (force && S < 2) S = 2;
+    return S < smax ? S : smax;
+}
+
 // HIP caps a launch at gridDim.x * blockDim.x < 2^32 threads: very tall problems run as
 // several launches over consecutive row ranges (each range is an independent GEMV).
 static int launch(int v, const double* A, int64_t lda, const double* x, double* y, int64_t M,
-                  int64_t K, hipStream_t s) {
+                  int64_t K, hipStream_t s, bool force_split) {
     const Variant& var = kVariants[v];
     const int64_t max_blocks = (1ll << 31) / var.threads;
+    if (var.split) {
+        int64_t S = split_count(var, M, K, force_split);
+        const int64_t ks = ((K + S - 1) / S + var.chunk - 1) / var.chunk * var.chunk;
+        S = (K + ks - 1) / ks;
+        const int64_t nrb = (M + var.rows_per_block - 1) / var.rows_per_block;
+        if (nrb * S > max_blocks) return fail(MVG_E_INVALID, "mvg_gemv: split-K grid too large");
+        double* partial = nullptr;
+        int rc = workspace(s, (size_t)(M * S), &partial);
+        if (rc != MVG_OK) return rc;
+        hipLaunchKernelGGL(var.split, dim3((unsigned)(nrb * S)), dim3(var.threads), 0, s, A, lda, x, partial, M,
+                           K, ks, S);
+        MVG_HIP(hipGetLastError());
+        const int64_t rblocks = (M + 255) / 256 < 4096 ? (M + 255) / 256 : 4096;
+        hipLaunchKernelGGL(gemv_splitk_reduce, dim3((unsigned)rblocks), dim3(256), 0, s, partial, S, y, M);
+        MVG_HIP(hipGetLastError());
+        return MVG_OK;
+    }
     const int64_t max_rows = max_blocks * var.rows_per_block;
     for (int64_t r0 = 0; r0 < M; r0 += max_rows) {
         const int64_t m = M - r0 < max_rows ? M - r0 : max_rows;
@@ -494,7 +607,7 @@ int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, i
     int v = variant == 0 ? pick_variant(lda, m, k, aligned) : variant;
     if (kVariants[v].vec && !(aligned && lda % 2 == 0))
         return fail(MVG_E_INVALID, "mvg_gemv: 16-B variant needs even lda and 16-B aligned A, x");
-    return launch(v, A, lda, x, y, m, k, s);
+    return launch(v, A, lda, x, y, m, k, s, variant != 0);
 }
 
 int mvg_gemv(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,

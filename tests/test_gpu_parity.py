@@ -37,7 +37,8 @@ def exact_dot(A, x):
 
 # ---------------------------------------------------------------- the raw kernel
 SHAPES = [(1, 1), (1, 2), (3, 5), (4, 8), (5, 7), (63, 129), (64, 128), (65, 127), (257, 1000), (1000, 257),
-          (33, 4096), (7, 20001), (2049, 512), (100, 1), (100, 2), (100, 3)]
+          (33, 4096), (7, 20001), (2049, 512), (100, 1), (100, 2), (100, 3),
+          (5, 40000), (130, 16388), (3, 65538)]
 
 
 @pytest.mark.parametrize("m,k", SHAPES)

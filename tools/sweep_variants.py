@@ -24,6 +24,10 @@ SHAPES = [
     ("mid_2097152x1024", 2097152, 1024),
     ("cfg5_full_4194304x512", 4194304, 512),
     ("cfg4_full_131072sq", 131072, 131072),
+    ("asym_120x60000", 120, 60000),
+    ("asym_1200x60000", 1200, 60000),
+    ("wide_64x1048576", 64, 1048576),
+    ("wide_1024x131072", 1024, 131072),
 ]
 
 
