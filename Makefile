@@ -18,7 +18,15 @@ HDRS     := $(CSRC)/common.h include/matvec_gpu.h
 OBJS     := $(BUILD)/gemv.o $(BUILD)/host.o $(BUILD)/engine.o $(BUILD)/textio.o
 APPS     := bin/multiplier_rowwise bin/multiplier_colwise bin/multiplier_blockwise
 
-all: $(LIB) $(APPS) oracle
+EXAMPLES := bin/rowwise_binding
+
+all: $(LIB) $(APPS) $(EXAMPLES) oracle
+
+examples: $(EXAMPLES)
+
+bin/rowwise_binding: examples/rowwise_binding.c $(LIB) include/matvec_gpu.h | $(BUILD)
+	gcc -O2 -std=c99 -D_POSIX_C_SOURCE=199309L -Wall -Wextra $< -o $@ -L$(PKG) -lmatvec_gpu -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
 
 $(BUILD):
 	mkdir -p $(BUILD) bin
@@ -43,7 +51,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APPS)
+	rm -rf $(BUILD) $(LIB) $(APPS) $(EXAMPLES)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle examples

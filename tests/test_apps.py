@@ -83,3 +83,18 @@ def test_synthetic_large_run(workdir):
     assert "device-resident" in r.stdout
     y = np.loadtxt(yout)
     assert max_rel(y, oracle.multiply("colwise", oracle.synth(R, C, 42), oracle.synth(1, C, 4242)[0], 1)) <= 1e-12
+
+
+def test_c_binding_example_is_plain_c():
+    # examples/rowwise_binding.c builds with gcc -std=c99 against the header
+    assert os.path.exists(os.path.join(REPO, "bin", "rowwise_binding"))
+
+
+@pytest.mark.gpu
+def test_c_binding_example_runs_the_fixture(workdir, golden):
+    r = subprocess.run([os.path.join(REPO, "bin", "rowwise_binding"), "4", "8", "1"], cwd=workdir,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    y = np.array([float(v) for v in r.stdout.split()])
+    assert max_rel(y, golden["fixture_4x8/rowwise/P1"]) <= 1e-12
+    assert re.fullmatch(r"4, 8, 1, \d+\.\d{6}\n", r.stderr.splitlines()[-1] + "\n")
