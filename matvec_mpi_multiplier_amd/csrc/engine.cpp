@@ -192,9 +192,17 @@ int mvg_comm_init_all(mvg_comm** out, int ndev, const int* devlist) {
     *out = nullptr;
     std::vector<int> devs(ndev);
     for (int i = 0; i < ndev; ++i) devs[i] = devlist ? devlist[i] : i;
-    std::vector<ncclComm_t> comms(ndev);
+    std::vector<ncclComm_t> comms(ndev, nullptr);
     DeviceGuard g;
-    MVG_NCCL(ncclCommInitAll(comms.data(), ndev, devs.data()));
+    // One device needs no collective (the exchange plan is empty), so RCCL is not initialised
+    // at all — no bootstrap cost, no RCCL banner on the executables' stdout — unless
+    // MVG_ALWAYS_COLLECT=1 asks for the collectives to run anyway.
+    const char* ac = getenv("MVG_ALWAYS_COLLECT");
+    if (ndev > 1 || (ac && ac[0] == '1')) {
+        MVG_NCCL(ncclCommInitAll(comms.data(), ndev, devs.data()));
+    } else {
+        MVG_HIP(hipSetDevice(devs[0]));
+    }
     mvg_comm* c = new mvg_comm;
     c->nranks = ndev;
     for (int i = 0; i < ndev; ++i) c->locals.push_back(LocalRank{i, devs[i], comms[i]});
