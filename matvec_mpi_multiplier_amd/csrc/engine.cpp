@@ -279,7 +279,9 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
     e->nranks = comm->nranks;
     e->single_process = (int)comm->locals.size() == comm->nranks;
     const char* ac = getenv("MVG_ALWAYS_COLLECT");
-    e->always_collect = ac && ac[0] == '1';
+    // forced collectives need an RCCL communicator (a one-device comm made without the
+    // variable has none)
+    e->always_collect = ac && ac[0] == '1' && comm->locals[0].comm != nullptr;
     e->shards.resize(comm->locals.size());
     auto bail = [&](int code) {
         mvg_engine_destroy(e);
