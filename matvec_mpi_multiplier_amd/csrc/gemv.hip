@@ -455,7 +455,7 @@ static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     if (!vec) return K >= 256 ? 9 : 10;
     if (K >= 8192) {
         // short, wide (the reference's 120..1200 x 60000 set): too few row workgroups -> split-K
-        if ((M + 1) / 2 < kSplitTarget / 2) return K >= 16384 ? 47 : 48;
+        if ((M + 1) / 2 < kSplitTarget / 2) return 48;
         if (K >= 16384) return M >= 32768 ? 41 : 32;
         return 42;
     }

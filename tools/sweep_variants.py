@@ -37,7 +37,7 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     max_elems = max(m * k for n, m, k in SHAPES if not only or n in only)
     buf = torch.empty(max_elems, dtype=torch.float64, device=dev)
-    xbuf = torch.empty(65536, dtype=torch.float64, device=dev)
+    xbuf = torch.empty(max(k for n, m, k in SHAPES if not only or n in only), dtype=torch.float64, device=dev)
     sink = torch.zeros(256 * 16 * 256, dtype=torch.float64, device=dev)
     nvar = lib.mvg_gemv_variant_count()
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
