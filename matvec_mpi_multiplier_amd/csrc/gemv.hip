@@ -441,11 +441,16 @@ constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
 constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4 per CU)
 
-// Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl):
-//   K >= 8192, fewer than 512 row workgroups: the same, split-K (deterministic two-pass)
-//   K >= 16384        row per workgroup, 4 waves x 2 rows, 8 x 16 B in flight per row per lane;
-//                     XCD-contiguous row ranges once there are >= 16384 workgroups (+0.3-0.8 %)
-//   8192 <= K < 16384 row per workgroup, 8 waves x 2 rows, XCD-contiguous (>= 2 chunks per wave)
+// Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl).
+// Long rows (K >= 8192), by the number of 2-row workgroups nrb = M/2:
+//   nrb < 512, or < 1024 with K < 98304: split-K, 4 waves x 2 rows x 512-col chunks (two-pass)
+//   nrb < 1024 (very long rows):         row per workgroup, 4 waves x 2 rows x 512-col chunks
+//   nrb < 8192:                          row per workgroup, 8 waves x 2 rows x 512-col chunks
+//   K >= 16384, nrb >= 8192:             4 waves x 2 rows x 1024-col chunks (218 VGPR: only
+//                                        worth it with many workgroups), XCD-contiguous rows
+//                                        from nrb >= 16384
+//   8192 <= K < 16384, nrb >= 8192:      8 waves x 2 rows x 512-col chunks, XCD-contiguous
+// Shorter rows:
 //   1536 < K < 8192   wave-owns-2-rows, pipelined + staggered start column
 //   768 < K <= 1536   wave-owns-4-rows, pipelined
 //   K <= 768          one row per wave (the whole row is one chunk: 524288 short waves stream
@@ -454,9 +459,11 @@ static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) return K >= 256 ? 9 : 10;
     if (K >= 8192) {
-        // short, wide (the reference's 120..1200 x 60000 set): too few row workgroups -> split-K
-        if ((M + 1) / 2 < kSplitTarget / 2) return 48;
-        if (K >= 16384) return M >= 32768 ? 41 : 32;
+        const int64_t nrb = (M + 1) / 2;
+        if (nrb < 512 || (nrb < 1024 && K < 98304)) return 48;
+        if (nrb < 1024) return 27;
+        if (nrb < 8192) return 24;
+        if (K >= 16384) return nrb >= 16384 ? 41 : 32;
         return 42;
     }
     if (K > 1536) return 15;

@@ -28,6 +28,11 @@ SHAPES = [
     ("asym_1200x60000", 1200, 60000),
     ("wide_64x1048576", 64, 1048576),
     ("wide_1024x131072", 1024, 131072),
+    ("mid_2048x65536", 2048, 65536),
+    ("mid_4096x16384", 4096, 16384),
+    ("mid_8192x16384", 8192, 16384),
+    ("mid_4096x32768", 4096, 32768),
+    ("mid_1536x32768", 1536, 32768),
 ]
 
 
