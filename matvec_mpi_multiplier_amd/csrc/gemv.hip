@@ -184,15 +184,16 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-// The workgroup's work: rows [row0, +RPB) over columns [0, K) of A/x (callers offset A and x
-// for a K-range); writes the row sums to out[r * out_stride].
-template <int NW, int RPB, int UNR, bool NT>
-__device__ __forceinline__ void rowblock_body(const double* __restrict__ A, int64_t lda,
-                                              const double* __restrict__ x, int64_t M, int64_t K,
-                                              int64_t row0, double* __restrict__ out,
-                                              int64_t out_stride, double (&part)[NW][RPB]) {
+template <int NW, int RPB, int UNR, bool NT, bool XCD = false>
+__global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
+                                                         const double* __restrict__ x,
+                                                         double* __restrict__ y, int64_t M,
+                                                         int64_t K) {
+    __shared__ double part[NW][RPB];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
+    const int64_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t row0 = bid * RPB;
     const double* arow[RPB];
 #pragma unroll
     for (int r = 0; r < RPB; ++r) {
@@ -253,19 +254,8 @@ __device__ __forceinline__ void rowblock_body(const double* __restrict__ A, int6
         double s = 0.0;
 #pragma unroll
         for (int v = 0; v < NW; ++v) s += part[v][threadIdx.x];
-        out[threadIdx.x * out_stride] = s;
+        y[row0 + threadIdx.x] = s;
     }
-}
-
-template <int NW, int RPB, int UNR, bool NT, bool XCD = false>
-__global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
-                                                         const double* __restrict__ x,
-                                                         double* __restrict__ y, int64_t M,
-                                                         int64_t K) {
-    __shared__ double part[NW][RPB];
-    const int64_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-    const int64_t row0 = bid * RPB;
-    rowblock_body<NW, RPB, UNR, NT>(A, lda, x, M, K, row0, y + row0, 1, part);
 }
 
 // Split-K for short, wide problems (few rows, so too few row workgroups to fill 256 CUs):
@@ -277,16 +267,80 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock_split(const double* __r
                                                                int64_t lda,
                                                                const double* __restrict__ x,
                                                                double* __restrict__ partial,
-                                                               int64_t M, int64_t K, int64_t ks,
+                                                               int64_t M, int64_t Kfull, int64_t ks,
                                                                int64_t S) {
     __shared__ double part[NW][RPB];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
     const int64_t rb = (int64_t)blockIdx.x / S;
     const int64_t sp = (int64_t)blockIdx.x % S;
     const int64_t k0 = sp * ks;
-    const int64_t k1 = k0 + ks < K ? k0 + ks : K;
+    const int64_t K = (k0 + ks < Kfull ? k0 + ks : Kfull) - k0;  // this workgroup's K-range
     const int64_t row0 = rb * RPB;
-    rowblock_body<NW, RPB, UNR, NT>(A + k0, lda, x + k0, M, k1 > k0 ? k1 - k0 : 0, row0,
-                                    partial + row0 * S + sp, S, part);
+    A += k0;
+    x += k0;
+    const double* arow[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    double acc[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) acc[r] = 0.0;
+
+    constexpr int64_t kStep = 128;            // columns per wave per sub-step (64 lanes x 2)
+    constexpr int64_t kChunk = kStep * UNR;
+    const int64_t nch = K / kChunk;
+    const int64_t c0 = 2 * lane;
+    int64_t i = w;
+    if (i < nch) {
+        dbl2 xa[UNR], xb[UNR];
+        dbl2 aa[RPB][UNR], ab[RPB][UNR];
+        load_chunk<RPB, UNR, NT>(arow, x, i * kChunk + c0, kStep, xa, aa);
+        for (; i + NW < nch; i += 2 * NW) {
+            load_chunk<RPB, UNR, NT>(arow, x, (i + NW) * kChunk + c0, kStep, xb, ab);
+            fma_chunk<RPB, UNR>(acc, xa, aa);
+            if (i + 2 * NW < nch) {
+                load_chunk<RPB, UNR, NT>(arow, x, (i + 2 * NW) * kChunk + c0, kStep, xa, aa);
+                fma_chunk<RPB, UNR>(acc, xb, ab);
+            } else {
+                fma_chunk<RPB, UNR>(acc, xb, ab);
+                i = nch;  // both buffers consumed
+                break;
+            }
+        }
+        if (i < nch) fma_chunk<RPB, UNR>(acc, xa, aa);
+    }
+    // column tail (K % kChunk), spread over the whole workgroup
+    for (int64_t c = nch * kChunk + 2 * (int64_t)threadIdx.x; c < K; c += 2 * NW * 64) {
+        if (c + 1 < K) {
+            const dbl2 xv = load2<false>(x + c);
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) {
+                const dbl2 a = load2<NT>(arow[r] + c);
+                acc[r] = __builtin_fma(a.x, xv.x, acc[r]);
+                acc[r] = __builtin_fma(a.y, xv.y, acc[r]);
+            }
+        } else {
+            const double xs = x[c];
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) acc[r] = __builtin_fma(arow[r][c], xs, acc[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        const double s = group_sum<64>(acc[r]);
+        if (lane == 0) part[w][r] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < RPB && row0 + threadIdx.x < M) {
+        double s = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += part[v][threadIdx.x];
+        partial[(row0 + threadIdx.x) * S + sp] = s;
+    }
 }
 
 __global__ void gemv_splitk_reduce(const double* __restrict__ partial, int64_t S,
