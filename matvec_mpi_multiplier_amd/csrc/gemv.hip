@@ -497,13 +497,12 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 
 // Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl).
 // Long rows (K >= 8192), by the number of 2-row workgroups nrb = M/2:
-//   nrb < 512, or < 1024 with K < 98304: split-K, 4 waves x 2 rows x 512-col chunks (two-pass)
-//   nrb < 1024 (very long rows):         row per workgroup, 4 waves x 2 rows x 512-col chunks
-//   nrb < 8192:                          row per workgroup, 8 waves x 2 rows x 512-col chunks
-//   K >= 16384, nrb >= 8192:             4 waves x 2 rows x 1024-col chunks (218 VGPR: only
-//                                        worth it with many workgroups), XCD-contiguous rows
-//                                        from nrb >= 16384
-//   8192 <= K < 16384, nrb >= 8192:      8 waves x 2 rows x 512-col chunks, XCD-contiguous
+//   nrb < 700            split-K, 4 waves x 2 rows x 512-col chunks (two-pass): 120 x 60000 in
+//                        13 us instead of 28, 1200 x 60000 at 6.5 TB/s instead of 5.9
+//   K >= 16384           4 waves x 2 rows x 1024-col chunks (218 VGPR, 8 x 16 B in flight per
+//                        row per lane), XCD-contiguous rows except 8192 <= nrb < 16384 (config
+//                        2's 16384^2 measures 0.7 % faster in dispatch order)
+//   8192 <= K < 16384    8 waves x 2 rows x 512-col chunks, XCD-contiguous
 // Shorter rows:
 //   1536 < K < 8192   wave-owns-2-rows, pipelined + staggered start column
 //   768 < K <= 1536   wave-owns-4-rows, pipelined
@@ -514,10 +513,8 @@ static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     if (!vec) return K >= 256 ? 9 : 10;
     if (K >= 8192) {
         const int64_t nrb = (M + 1) / 2;
-        if (nrb < 512 || (nrb < 1024 && K < 98304)) return 48;
-        if (nrb < 1024) return 27;
-        if (nrb < 8192) return 24;
-        if (K >= 16384) return nrb >= 16384 ? 41 : 32;
+        if (nrb < 700) return 48;
+        if (K >= 16384) return (nrb >= 8192 && nrb < 16384) ? 32 : 41;
         return 42;
     }
     if (K > 1536) return 15;
