@@ -184,7 +184,19 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-template <int NW, int RPB, int UNR, bool NT, bool XCD = false>
+// Chunked XCD order: XCD k takes runs of Q consecutive workgroups, the 8 XCDs' runs side by
+// side, so each XCD still streams contiguous memory while all of them stay inside one sliding
+// window (the full-range remap above puts the XCDs' streams R/8 rows apart, a power-of-two
+// distance for power-of-two shapes). Identity on the tail that does not fill 8*Q.
+template <int Q>
+__device__ __forceinline__ int64_t xcd_chunk_remap(int64_t b, int64_t nwg) {
+    const int64_t full = nwg / (8 * Q) * (8 * Q);
+    if (b >= full) return b;
+    const int64_t xcd = b % 8, j = b / 8;
+    return ((j / Q) * 8 + xcd) * Q + j % Q;
+}
+
+template <int NW, int RPB, int UNR, bool NT, int XCD = 0>
 __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restrict__ A, int64_t lda,
                                                          const double* __restrict__ x,
                                                          double* __restrict__ y, int64_t M,
@@ -192,7 +204,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restric
     __shared__ double part[NW][RPB];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    int64_t bid = blockIdx.x;
+    if constexpr (XCD == 1) bid = xcd_remap(bid, gridDim.x);
+    if constexpr (XCD > 1) bid = xcd_chunk_remap<XCD>(bid, gridDim.x);
     const int64_t row0 = bid * RPB;
     const double* arow[RPB];
 #pragma unroll
@@ -435,7 +449,9 @@ struct Variant {
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_splitk", nullptr, RPB, true, NW * 64,                \
      gemv_rowblock_split<NW, RPB, UNR, true>, 128 * UNR}
 #define RWX(NW, RPB, UNR)                                                                  \
-    {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xcd", gemv_rowblock<NW, RPB, UNR, true, true>, RPB, true, NW * 64}
+    {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xcd", gemv_rowblock<NW, RPB, UNR, true, 1>, RPB, true, NW * 64}
+#define RWQ(NW, RPB, UNR, Q)                                                               \
+    {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xq" #Q, gemv_rowblock<NW, RPB, UNR, true, Q>, RPB, true, NW * 64}
 
 static const Variant kVariants[] = {
     {"auto", nullptr, 0, false},   // 0
@@ -490,6 +506,11 @@ static const Variant kVariants[] = {
     RWS(4, 1, 8),                  // 49
     RWS(8, 1, 4),                  // 50
     RWS(4, 1, 4),                  // 51
+    RWQ(4, 2, 8, 16),              // 52 chunked XCD order
+    RWQ(4, 2, 8, 64),              // 53
+    RWQ(4, 2, 8, 256),             // 54
+    RWQ(8, 2, 4, 64),              // 55
+    RWQ(4, 2, 8, 4),               // 56
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 

@@ -33,6 +33,7 @@ SHAPES = [
     ("mid_8192x16384", 8192, 16384),
     ("mid_4096x32768", 4096, 32768),
     ("mid_1536x32768", 1536, 32768),
+    ("cfg3_g1_65536sq", 65536, 65536),
 ]
 
 
