@@ -521,9 +521,10 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 //   nrb < 700            split-K, 4 waves x 2 rows x 512-col chunks (two-pass): 120 x 60000 in
 //                        13 us instead of 28, 1200 x 60000 at 6.5 TB/s instead of 5.9
 //   K >= 16384           4 waves x 2 rows x 1024-col chunks (218 VGPR, 8 x 16 B in flight per
-//                        row per lane), XCD-contiguous rows except 8192 <= nrb < 16384 (config
-//                        2's 16384^2 measures 0.7 % faster in dispatch order)
-//   8192 <= K < 16384    8 waves x 2 rows x 512-col chunks, XCD-contiguous
+//                        row per lane)
+//   8192 <= K < 16384    8 waves x 2 rows x 512-col chunks
+// Workgroups run in dispatch order: XCD-contiguous orders win <= 1.3 % on some shapes but lose
+// 5 % at 131072^2, where the 8 XCDs' streams land 2^34 B apart (variant_sweep11_xcd.jsonl).
 // Shorter rows:
 //   1536 < K < 8192   wave-owns-2-rows, pipelined + staggered start column
 //   768 < K <= 1536   wave-owns-4-rows, pipelined
@@ -535,8 +536,7 @@ static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     if (K >= 8192) {
         const int64_t nrb = (M + 1) / 2;
         if (nrb < 700) return 48;
-        if (K >= 16384) return (nrb >= 8192 && nrb < 16384) ? 32 : 41;
-        return 42;
+        return K >= 16384 ? 32 : 24;
     }
     if (K > 1536) return 15;
     if (K > 768) return 11;
