@@ -138,8 +138,12 @@ def main():
     value = total_bytes * args.steps / elapsed / 1e9
     achieved = per_gpu / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
 
-    # quick parity guard on the timed result (rank 0: sampled rows vs the closed form)
+    # y of the timed steps, on rank 0: every element must lie in [0, C * 0.9999^2] (inputs are in
+    # [0, 0.9999]); exact parity is checked against the reference restatement in cpu_baseline
+    # (N = 1) and by tests/.
     y = eng.collect()
+    if rank == 0:
+        assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, "y out of range"
 
     # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
     e2e = None
