@@ -212,6 +212,11 @@ int mvg_engine_destroy(mvg_engine* e);
 int mvg_matrix_filename(int64_t R, int64_t C, char* buf, size_t buflen);
 int mvg_vector_filename(int64_t n, char* buf, size_t buflen);
 int mvg_load_matr(const char* dir, int64_t R, int64_t C, double* A);
+/* Binary cache beside the text (<dir>/matrix_<R>_<C>.bin: "MVGBIN1\0", int64 R, int64 C, R*C
+ * native fp64). mvg_load_matr reads it instead of the text when it exists, matches (R, C) and is
+ * not older than the text; with MVG_BIN_CACHE=1 it also writes it after parsing the text;
+ * MVG_BIN_CACHE=0 ignores it. Parsing a 30-120 GB text file once is then enough. */
+int mvg_write_matr_bin(const char* path, const double* A, int64_t R, int64_t C);
 int mvg_load_vec(const char* dir, int64_t n, double* x);
 int mvg_write_vec(const char* path, const double* v, int64_t n);   /* "%.17g\n" per value */
 int mvg_write_matr_synth(const char* path, int64_t R, int64_t C, uint64_t seed); /* "%.4f " */

@@ -125,6 +125,7 @@ SIGNATURES = {
     "mvg_matrix_filename": (C.c_int, [_i64, _i64, C.c_char_p, C.c_size_t]),
     "mvg_vector_filename": (C.c_int, [_i64, C.c_char_p, C.c_size_t]),
     "mvg_load_matr": (C.c_int, [C.c_char_p, _i64, _i64, _p]),
+    "mvg_write_matr_bin": (C.c_int, [C.c_char_p, _p, _i64, _i64]),
     "mvg_load_vec": (C.c_int, [C.c_char_p, _i64, _p]),
     "mvg_write_vec": (C.c_int, [C.c_char_p, _p, _i64]),
     "mvg_write_matr_synth": (C.c_int, [C.c_char_p, _i64, _i64, C.c_uint64]),

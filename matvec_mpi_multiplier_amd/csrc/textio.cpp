@@ -133,6 +133,55 @@ int parse_file(const std::string& path, int64_t n, double* out) {
     return MVG_OK;
 }
 
+// ---- binary cache: "MVGBIN1\0", int64 rows, int64 cols, rows*cols native fp64 (row-major)
+constexpr char kMagic[8] = {'M', 'V', 'G', 'B', 'I', 'N', '1', '\0'};
+constexpr size_t kHeader = 24;
+
+// Reads the cache into out if it exists, matches (R, C) and is at least as new as the text
+// file (when the text exists). Returns MVG_OK, or MVG_E_IO when there is no usable cache.
+int read_bin(const std::string& bin, const std::string& txt, int64_t R, int64_t C, double* out) {
+    struct stat sb, st;
+    if (stat(bin.c_str(), &sb) != 0) return MVG_E_IO;
+    if (stat(txt.c_str(), &st) == 0 && st.st_mtime > sb.st_mtime) return MVG_E_IO;  // stale
+    const size_t n = (size_t)R * (size_t)C;
+    if ((size_t)sb.st_size != kHeader + n * sizeof(double)) return MVG_E_IO;
+    int fd = open(bin.c_str(), O_RDONLY);
+    if (fd < 0) return MVG_E_IO;
+    char hdr[kHeader];
+    if (pread(fd, hdr, kHeader, 0) != (ssize_t)kHeader || memcmp(hdr, kMagic, 8) != 0) {
+        close(fd);
+        return MVG_E_IO;
+    }
+    int64_t r, c;
+    memcpy(&r, hdr + 8, 8);
+    memcpy(&c, hdr + 16, 8);
+    if (r != R || c != C) {
+        close(fd);
+        return MVG_E_IO;
+    }
+    std::vector<int> bad(64, 0);
+    const size_t bytes = n * sizeof(double);
+    parallel_for((int64_t)((bytes + (64u << 20) - 1) / (64u << 20)), [&](int64_t a, int64_t b) {
+        for (int64_t blk = a; blk < b; ++blk) {
+            size_t off = (size_t)blk * (64u << 20);
+            size_t len = std::min<size_t>(64u << 20, bytes - off);
+            char* dst = (char*)out + off;
+            while (len > 0) {
+                const ssize_t got = pread(fd, dst, len, (off_t)(kHeader + off));
+                if (got <= 0) {
+                    bad[0] = 1;
+                    return;
+                }
+                dst += got;
+                off += (size_t)got;
+                len -= (size_t)got;
+            }
+        }
+    }, bytes < (64u << 20));
+    close(fd);
+    return bad[0] ? MVG_E_IO : MVG_OK;
+}
+
 std::string join(const char* dir, const std::string& name) {
     std::string d = dir ? dir : ".";
     if (!d.empty() && d.back() != '/') d += '/';
@@ -159,7 +208,33 @@ int mvg_load_matr(const char* dir, int64_t R, int64_t C, double* A) {
     if (R < 0 || C < 0 || (!A && R * C > 0)) return fail(MVG_E_INVALID, "mvg_load_matr: bad arguments");
     char name[128];
     mvg_matrix_filename(R, C, name, sizeof name);
-    return parse_file(join(dir, name), R * C, A);
+    const std::string txt = join(dir, name);
+    std::string bin = txt.substr(0, txt.size() - 4) + ".bin";
+    const char* mode = getenv("MVG_BIN_CACHE");  // unset: use a cache if present; "1": also write; "0": off
+    const bool use = !(mode && mode[0] == '0');
+    if (use && R * C > 0 && read_bin(bin, txt, R, C, A) == MVG_OK) return MVG_OK;
+    int rc = parse_file(txt, R * C, A);
+    if (rc == MVG_OK && mode && mode[0] == '1') rc = mvg_write_matr_bin(bin.c_str(), A, R, C);
+    return rc;
+}
+
+int mvg_write_matr_bin(const char* path, const double* A, int64_t R, int64_t C) {
+    if (!path || R < 0 || C < 0 || (!A && R * C > 0)) return fail(MVG_E_INVALID, "mvg_write_matr_bin: bad arguments");
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return fail(MVG_E_IO, "Unable to create '" + tmp + "'");
+    bool ok = fwrite(kMagic, 1, 8, f) == 8 && fwrite(&R, 8, 1, f) == 1 && fwrite(&C, 8, 1, f) == 1;
+    const size_t n = (size_t)R * (size_t)C;
+    for (size_t off = 0; ok && off < n; off += (size_t)1 << 24) {
+        const size_t len = std::min<size_t>((size_t)1 << 24, n - off);
+        ok = fwrite(A + off, sizeof(double), len, f) == len;
+    }
+    ok = (fclose(f) == 0) && ok;
+    if (!ok || rename(tmp.c_str(), path) != 0) {
+        remove(tmp.c_str());
+        return fail(MVG_E_IO, std::string("write failed for '") + path + "'");
+    }
+    return MVG_OK;
 }
 
 int mvg_load_vec(const char* dir, int64_t n, double* x) {

@@ -81,6 +81,12 @@ def write_vec(path: str, v: np.ndarray) -> None:
     check(lib.mvg_write_vec(path.encode(), v.ctypes.data, v.size), "write_vec")
 
 
+def write_matr_bin(path: str, A: np.ndarray) -> None:
+    """The binary cache load_matr prefers over the text when present (see matvec_gpu.h)."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    check(lib.mvg_write_matr_bin(path.encode(), A.ctypes.data, A.shape[0], A.shape[1]), "write_matr_bin")
+
+
 def write_matr_synth(path: str, R: int, Cn: int, seed: int) -> None:
     check(lib.mvg_write_matr_synth(path.encode(), R, Cn, seed), "write_matr_synth")
 
