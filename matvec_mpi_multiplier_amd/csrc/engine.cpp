@@ -514,9 +514,12 @@ int mvg_engine_multiply(mvg_engine* e) {
         if (rc != MVG_OK) return rc;
         if (timed) MVG_HIP(hipEventRecord(t1, s.stream));
     }
-    // 2) the exchange step, from the shared schedule (mvg_plan_exchange)
+    // 2) the exchange step, from the shared schedule (mvg_plan_exchange). A failing call inside
+    // the group still closes the group before the error is reported.
     for (int k = 0; k < nsteps; ++k) {
         MVG_NCCL(ncclGroupStart());
+        ncclResult_t r = ncclSuccess;
+        const char* what = "";
         for (auto& s : e->shards) {
             const mvg_xstep& st = s.steps[k];
             if (!st.member) continue;
@@ -526,12 +529,17 @@ int mvg_engine_multiply(mvg_engine* e) {
             double* dst = bufs[st.dst];
             if (!dst) dst = s.dy_part;  // recvbuff is only written on the root
             if (st.op == MVG_X_GATHER) {
-                MVG_NCCL(ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], s.stream));
+                r = ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], s.stream);
+                what = "ncclGather";
             } else {
-                MVG_NCCL(ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], s.stream));
+                r = ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], s.stream);
+                what = "ncclReduce";
             }
+            if (r != ncclSuccess) break;
         }
-        MVG_NCCL(ncclGroupEnd());
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return nccl_fail(r, what);
+        if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
     }
     return MVG_OK;
 }
