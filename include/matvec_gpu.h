@@ -152,6 +152,13 @@ int mvg_gemv_variant_count(void);
 int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k);
 const char* mvg_gemv_variant_name(int variant);
 
+/* Several x per pass over A (beyond the reference's surface):
+ * Y[:, v] = A X[:, v] for v < nv, X k x nv and Y m x nv column-major (vector v at X + v*ldx,
+ * Y + v*ldy; ldx >= k, ldy >= m). A is streamed once per group of 8 vectors, so the HBM cost
+ * of nv products approaches that of one. Same numerics contract as mvg_gemv. */
+int mvg_gemv_multi(const double* d_A, int64_t lda, const double* d_X, int64_t ldx, double* d_Y,
+                   int64_t ldy, int64_t m, int64_t k, int nv, void* stream);
+
 /* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */
 int mvg_stream_read(const double* d_src, int64_t n, double* d_sink, void* stream);
 

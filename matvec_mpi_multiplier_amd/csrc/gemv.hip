@@ -609,6 +609,99 @@ static int launch(int v, const double* A, int64_t lda, const double* x, double* 
     return MVG_OK;
 }
 
+// ------------------------------------------------------------------ several x per pass
+// Y[:, v] = A X[:, v] for v < nv (nv <= NV): the row-per-workgroup stream of A with NV x
+// vectors consumed per A chunk, so A is read once for all of them. X and Y
+// are column-major (vector v at X + v*ldx, Y + v*ldy). Vectors v >= nv alias vector 0 and are
+// never stored. Per-wave sums meet in LDS and are added in wave order (deterministic).
+template <int NW, int RPB, int UNR, int NV>
+__global__ __launch_bounds__(NW * 64) void gemv_multi(const double* __restrict__ A, int64_t lda,
+                                                      const double* __restrict__ X, int64_t ldx,
+                                                      double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                      int64_t K, int nv) {
+    __shared__ double part[NW][RPB][NV];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t row0 = (int64_t)blockIdx.x * RPB;
+    const double* arow[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    const double* xv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xv[v] = X + (v < nv ? v : 0) * ldx;
+    double acc[RPB][NV];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[r][v] = 0.0;
+
+    constexpr int64_t kStep = 128;
+    constexpr int64_t kChunk = kStep * UNR;
+    const int64_t nch = K / kChunk;
+    const int64_t c0 = 2 * lane;
+    for (int64_t i = w; i < nch; i += NW) {
+        const int64_t base = i * kChunk + c0;
+        dbl2 a[RPB][UNR];
+#pragma unroll
+        for (int r = 0; r < RPB; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) a[r][u] = load2<true>(arow[r] + base + u * kStep);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            dbl2 xx[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) xx[u] = load2<false>(xv[v] + base + u * kStep);
+#pragma unroll
+            for (int r = 0; r < RPB; ++r)
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    acc[r][v] = __builtin_fma(a[r][u].x, xx[u].x, acc[r][v]);
+                    acc[r][v] = __builtin_fma(a[r][u].y, xx[u].y, acc[r][v]);
+                }
+        }
+    }
+    for (int64_t c = nch * kChunk + 2 * (int64_t)threadIdx.x; c < K; c += 2 * NW * 64) {
+        if (c + 1 < K) {
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) {
+                const dbl2 a = load2<true>(arow[r] + c);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    const dbl2 xx = load2<false>(xv[v] + c);
+                    acc[r][v] = __builtin_fma(a.x, xx.x, acc[r][v]);
+                    acc[r][v] = __builtin_fma(a.y, xx.y, acc[r][v]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < RPB; ++r)
+#pragma unroll
+                for (int v = 0; v < NV; ++v) acc[r][v] = __builtin_fma(arow[r][c], xv[v][c], acc[r][v]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPB; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const double s = group_sum<64>(acc[r][v]);
+            if (lane == 0) part[w][r][v] = s;
+        }
+    __syncthreads();
+    for (int t = threadIdx.x; t < RPB * NV; t += NW * 64) {
+        const int r = t / NV, v = t % NV;
+        if (row0 + r < M && v < nv) {
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) s += part[q][r][v];
+            Y[v * ldy + row0 + r] = s;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ other kernels
 __global__ void zero_kernel(double* y, int64_t m) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
@@ -692,6 +785,41 @@ int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, i
 int mvg_gemv(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
              void* stream) {
     return mvg_gemv_variant(A, lda, x, y, m, k, 0, stream);
+}
+
+int mvg_gemv_multi(const double* A, int64_t lda, const double* X, int64_t ldx, double* Y, int64_t ldy,
+                   int64_t m, int64_t k, int nv, void* stream) {
+    if (m < 0 || k < 0 || nv < 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: negative size");
+    if (m == 0 || nv == 0) return MVG_OK;
+    if (!A || !X || !Y || lda < k || ldx < k || ldy < m)
+        return fail(MVG_E_INVALID, "mvg_gemv_multi: null pointer or leading dimension too small");
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)X % 16 == 0) && lda % 2 == 0 && ldx % 2 == 0;
+    if (!vec || k == 0) {  // the 8-B path: one vector at a time
+        for (int v = 0; v < nv; ++v) {
+            int rc = mvg_gemv_variant(A, lda, X + v * ldx, Y + v * ldy, m, k, vec ? 0 : 9, stream);
+            if (rc != MVG_OK) return rc;
+        }
+        return MVG_OK;
+    }
+    constexpr int NW = 8, RPB = 2;
+    const int64_t blocks = (m + RPB - 1) / RPB;
+    if (blocks > (1ll << 31) / (NW * 64)) return fail(MVG_E_INVALID, "mvg_gemv_multi: too many rows");
+    for (int v0 = 0; v0 < nv; v0 += 8) {  // groups of <= 8 vectors per pass over A
+        const int g = nv - v0 < 8 ? nv - v0 : 8;
+        const double* Xg = X + v0 * ldx;
+        double* Yg = Y + v0 * ldy;
+        if (g == 1)
+            hipLaunchKernelGGL((gemv_multi<NW, RPB, 4, 1>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
+        else if (g == 2)
+            hipLaunchKernelGGL((gemv_multi<NW, RPB, 4, 2>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
+        else if (g <= 4)
+            hipLaunchKernelGGL((gemv_multi<NW, RPB, 2, 4>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
+        else
+            hipLaunchKernelGGL((gemv_multi<NW, RPB, 2, 8>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
+        MVG_HIP(hipGetLastError());
+    }
+    return MVG_OK;
 }
 
 int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {

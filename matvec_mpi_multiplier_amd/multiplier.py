@@ -139,6 +139,23 @@ def gemv(d_A: int, lda: int, d_x: int, d_y: int, m: int, k: int, stream=None, va
     check(lib.mvg_gemv_variant(d_A, lda, d_x, d_y, m, k, variant, stream), "mvg_gemv")
 
 
+def multiply_multi(A: np.ndarray, X: np.ndarray) -> np.ndarray:
+    """Y = A X for a k x nv block of vectors in one pass over A (mvg_gemv_multi); returns m x nv."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    X = np.asarray(X, dtype=np.float64)
+    R, Cn = A.shape
+    nv = X.shape[1]
+    Xc = np.ascontiguousarray(X.T)  # column-major: vector v contiguous
+    dA, dX, dY = DeviceBuffer(R * Cn).upload(A), DeviceBuffer(Cn * nv).upload(Xc), DeviceBuffer(R * nv)
+    try:
+        check(lib.mvg_gemv_multi(dA.ptr, Cn, dX.ptr, Cn, dY.ptr, R, R, Cn, nv, None), "mvg_gemv_multi")
+        check(lib.mvg_stream_sync(None), "sync")
+        return dY.download(R * nv).reshape(nv, R).T.copy()
+    finally:
+        for b in (dA, dX, dY):
+            b.free()
+
+
 def multiply_std_rowwise(A: np.ndarray, x: np.ndarray, variant: int = 0) -> np.ndarray:
     """src/matr_utils.c:86-96 on the GPU: copies A, x to the current device, runs the HIP
     GEMV, returns y. Matches the reference's sequential sum to <= 1e-12 relative."""

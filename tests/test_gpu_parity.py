@@ -273,3 +273,14 @@ def test_auto_variant_names_match_the_dispatch_table():
     pick = lambda m, k: _lib.lib.mvg_gemv_variant_name(_lib.lib.mvg_gemv_auto_variant(k, m, k)).decode()
     assert pick(120, 60000) == "rowblk_w4_r2_u4_splitk" and pick(1024, 131072) == "rowblk_w4_r2_u4_splitk"
     assert pick(4096, 16384) == "rowblk_w4_r2_u8" and pick(1536, 32768) == "rowblk_w4_r2_u8"
+
+
+@pytest.mark.parametrize("m,k,nv", [(257, 1000, 1), (64, 16384, 2), (130, 4096, 3), (33, 20000, 5), (9, 512, 8),
+                                    (100, 3000, 11), (50, 1001, 4)])
+def test_multi_vector_gemv(m, k, nv):
+    A = oracle.synth(m, k, 42)
+    X = oracle.synth(nv, k, 4242).T  # k x nv
+    Y = mm.multiply_multi(A, X)
+    assert Y.shape == (m, nv)
+    for v in range(nv):
+        assert max_rel(Y[:, v], oracle.multiply_std_rowwise(A, np.ascontiguousarray(X[:, v]))) <= TOL, v
