@@ -175,7 +175,7 @@ int main(int argc, char** argv) {
         sum_time += now_s() - t0;
     }
     // device-resident: A already on the GPUs; GEMV + exchange only
-    mvg_engine_kernel_timing(eng, 1);
+    mvg_engine_kernel_timing(eng, 5);  // events on every 5th multiply (each pair costs ~6 us)
     const double t0 = now_s();
     for (long it = 0; it < iters; ++it)
         if ((rc = mvg_engine_multiply(eng)) != MVG_OK) return die(rc, "multiply");
