@@ -300,12 +300,14 @@ def cpu_baseline(args, R, C, y_gpu):
     rows = R
     if R * C * 8 > args.cpu_sample_bytes:
         rows = max(1, int(args.cpu_sample_bytes // (C * 8)))
-    # keep the sample splittable the way the algorithm splits it over `threads` ranks
-    while threads > 1 and not _splits(args.alg, rows, C, threads):
-        threads -= 1
-    if args.alg in ("rowwise", "blockwise"):
+    # keep the sample splittable the way the algorithm splits it over `threads` ranks: sampled
+    # rows are rounded down to a multiple of the ranks over rows; the column split (fixed C)
+    # lowers the rank count instead
+    if rows < R and args.alg in ("rowwise", "blockwise"):
         gr = oracle.grid_shape(threads)[0] if args.alg == "blockwise" else threads
         rows = max(gr, rows - rows % gr)
+    while threads > 1 and not _splits(args.alg, rows, C, threads):
+        threads -= 1
     A = oracle.synth_block(0, rows, 0, C, C, 42)
     x = oracle.synth(1, C, 4242)[0]
     t1, y_cpu = oracle.time_multiply(args.alg, A, x, threads, 1)
