@@ -233,35 +233,17 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
                 "GBps": total_bytes / float(np.mean(times)) / 1e9}
 
     out = {"semantics": "reference: root holds A, x in host memory; distribute + multiply + y on root"}
-    nbytes = R * C * 8
-    shm = None
+    from matvec_mpi_multiplier_amd.hostshare import SharedHostMatrix, shm_free_bytes
+
+    shared = None
     if not distributed:
         A = mm.synth_host(R, C, 42)
     else:
-        A = None
-        from multiprocessing import resource_tracker, shared_memory
-
-        name = f"mvg_bench_{os.environ.get('MASTER_PORT', '0')}"
-        free = 0
-        try:
-            st = os.statvfs("/dev/shm")
-            free = st.f_bavail * st.f_frsize
-        except OSError:
-            pass
-        ok = torch.tensor([1 if free > nbytes + (1 << 30) else 0], device=f"cuda:{local}")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok[0]):
-            if rank == 0:
-                shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
-                A = np.ndarray((R, C), dtype=np.float64, buffer=shm.buf)
-                _l.mvg_synth_fill_host(A.ctypes.data, C, R, C, 0, 0, C, 42)
-            barrier()
-            if rank != 0:
-                shm = shared_memory.SharedMemory(name=name)
-                resource_tracker.unregister(shm._name, "shared_memory")
-                A = np.ndarray((R, C), dtype=np.float64, buffer=shm.buf)
-        else:
-            out["shared"] = f"skipped: /dev/shm has {free >> 30} GiB free, needs {nbytes >> 30} GiB"
+        shared = SharedHostMatrix.create(R, C, 42, f"bench_{os.environ.get('MASTER_PORT', '0')}",
+                                         device=f"cuda:{local}")
+        A = shared.array if shared is not None else None
+        if shared is None:
+            out["shared"] = f"skipped: /dev/shm has {shm_free_bytes() >> 30} GiB free, needs {(R * C * 8) >> 30} GiB"
     x = mm.synth_host(1, C, 4242)[0]
     have_shared = A is not None
     if distributed and not have_shared and rank == 0:
@@ -277,16 +259,10 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
         out["root_send"]["distribution"] = "root H2D staging + ncclSend over xGMI"
     if pinned:
         _l.mvg_host_unregister(A.ctypes.data)
-    if shm is not None:
-        barrier()
+    if shared is not None:
         eng._keep = None
         del A
-        try:
-            shm.close()
-        except BufferError:
-            pass
-        if rank == 0:
-            shm.unlink()
+        shared.close()
     return out
 
 

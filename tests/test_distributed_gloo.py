@@ -132,3 +132,45 @@ def test_gloo_exchange_replay_matches_reference(golden, case, R, C, alg, P, exac
         np.testing.assert_array_equal(y, want)
     else:  # gloo's reduce order for > 2 ranks is its own (MPICH/RCCL differ too)
         assert max_rel(y, want) <= 1e-15
+
+
+def _shm_worker(rank, world, port, R, C, outq):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd.hostshare import SharedHostMatrix
+    from oracle import oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sh = SharedHostMatrix.create(R, C, 42, f"test_{port}", margin=0)
+        assert sh is not None
+        # every rank sees rank 0's synthetic matrix; each checks the rows its shard would pull
+        lo, hi = rank * R // world, (rank + 1) * R // world
+        np.testing.assert_array_equal(sh.array[lo:hi], oracle.synth_block(lo, hi - lo, 0, C, C, 42))
+        sh.close()
+        outq.put((rank, "ok"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_host_matrix_two_ranks():
+    """bench.py's end-to-end `shared` distribution: rank 0 creates the root's A in /dev/shm,
+    rank 1 maps the same bytes, both unmap, the segment is removed (no leak)."""
+    from matvec_mpi_multiplier_amd.hostshare import shm_free_bytes
+
+    if shm_free_bytes() < (64 << 20):
+        pytest.skip("/dev/shm too small here")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shm_worker, args=(r, 2, port, 96, 80, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [(0, "ok"), (1, "ok")]
+    assert not os.path.exists(f"/dev/shm/mvg_test_{port}")
