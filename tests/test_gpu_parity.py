@@ -284,3 +284,30 @@ def test_multi_vector_gemv(m, k, nv):
     assert Y.shape == (m, nv)
     for v in range(nv):
         assert max_rel(Y[:, v], oracle.multiply_std_rowwise(A, np.ascontiguousarray(X[:, v]))) <= TOL, v
+
+
+def test_distribute_shared_from_dev_shm(comm1, golden, tmp_path):
+    """bench.py's N > 1 'shared' end-to-end path at world size 1: A in a /dev/shm segment,
+    pinned with hipHostRegister, pulled by the GPU, y vs the reference's golden y."""
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd.hostshare import SharedHostMatrix
+
+    dist.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        sh = SharedHostMatrix.create(480, 480, 42, f"gputest_{os.getpid()}", margin=0)
+        assert sh is not None
+        A = sh.array
+        x = oracle.synth(1, 480, 4242)[0]
+        assert _lib.lib.mvg_host_register(A.ctypes.data, A.nbytes) == 0
+        with mm.Multiplier("colwise", 480, 480, comm1) as e:
+            e.distribute_shared(A, x)
+            e.multiply()
+            y = e.collect()
+            e._keep = None
+        _lib.lib.mvg_host_unregister(A.ctypes.data)
+        del A
+        sh.close()
+        assert max_rel(y, golden["sq_480/colwise/P1"]) <= TOL
+    finally:
+        dist.destroy_process_group()
