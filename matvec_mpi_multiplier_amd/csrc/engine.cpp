@@ -160,34 +160,15 @@ inline int64_t x_len(const mvg_shard& p) { return p.n_cols; }
 
 // Every local device pulls its own shard (and x segment) from host memory that holds the
 // whole A and x, over its own PCIe link, concurrently (one stream per device).
-// MVG_H2D_STREAMS=n (1..4, default 1) splits each shard's copy into n row ranges issued on
-// n streams (the engine stream and its copy stream alternate), for more than one DMA engine.
 int distribute_direct(mvg_engine* e, const double* A, const double* x) {
     const int64_t C = e->C;
-    int nsplit = 1;
-    if (const char* v = getenv("MVG_H2D_STREAMS")) nsplit = atoi(v);
-    if (nsplit < 1) nsplit = 1;
-    if (nsplit > 4) nsplit = 4;
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
         const mvg_shard& p = s.plan;
-        const int64_t per = (p.n_rows + nsplit - 1) / nsplit;
-        for (int i = 0; i < nsplit; ++i) {
-            const int64_t r0 = i * per, r1 = std::min(p.n_rows, r0 + per);
-            if (r1 <= r0) break;
-            hipStream_t st = (i % 2 == 0) ? s.stream : s.copy_stream;
-            int rc = h2d_region(s.dA + r0 * p.n_cols, A + (p.row_off + r0) * C + p.col_off, C, r1 - r0, p.n_cols, st);
-            if (rc != MVG_OK) return rc;
-        }
-        int rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
+        int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
         if (rc != MVG_OK) return rc;
-        if (nsplit > 1) {  // the multiply on s.stream must see the copy stream's rows
-            hipEvent_t ev;
-            MVG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            MVG_HIP(hipEventRecord(ev, s.copy_stream));
-            MVG_HIP(hipStreamWaitEvent(s.stream, ev, 0));
-            MVG_HIP(hipEventDestroy(ev));
-        }
+        rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
+        if (rc != MVG_OK) return rc;
     }
     return MVG_OK;
 }
