@@ -58,7 +58,8 @@ def main():
         ref = torch.mv(A, x)
         nbytes = 8 * (M * K + K + M)
         results = {}
-        variants = [v for v in range(nvar) if lib.mvg_gemv_variant_name(v).startswith((b"vec", b"rowblk"))] + [0]
+        prefixes = tuple(p.encode() for p in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["vec", "rowblk"]))
+        variants = [v for v in range(nvar) if lib.mvg_gemv_variant_name(v).startswith(prefixes)] + [0]
         y = torch.empty(M, dtype=torch.float64, device=dev)
         for v in variants:
             y.zero_()
