@@ -187,7 +187,9 @@ int mvg_comm_destroy(mvg_comm* c);
  *   multiply   : local GEMV on every device + the exchange step
  *                (row: ncclGather of y; col: ncclReduce(SUM); block: ncclReduce(SUM) on each
  *                 grid-row communicator, then ncclGather of the row leaders' slices).
- *                Asynchronous on the engine's streams; mvg_engine_sync waits.
+ *                Asynchronous on the engine's streams; mvg_engine_sync waits. The exchange
+ *                runs on a second stream per device and overlaps the next multiply's GEMV
+ *                (partial y double-buffered); collect and sync wait for it.
  *   collect    : y (R doubles) -> host on the root.  */
 typedef struct mvg_engine mvg_engine;
 int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm* comm);
@@ -202,7 +204,8 @@ int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x);
 int mvg_engine_multiply(mvg_engine* e);
 int mvg_engine_sync(mvg_engine* e);
 int mvg_engine_collect(mvg_engine* e, double* y_host);
-/* per-local-device stream (hipStream_t as void*), e.g. for hipEvent timing by the caller */
+/* per-local-device GEMV stream (hipStream_t as void*), e.g. for hipEvent timing of the GEMV by
+ * the caller; y on the root is complete only after mvg_engine_sync / mvg_engine_collect */
 int mvg_engine_stream(const mvg_engine* e, int local_index, void** stream);
 /* Average GEMV kernel time (ms) over the multiply calls since the last reset, measured with
  * hipEvents bracketing the kernel on each local device's stream (max over local devices).

@@ -60,6 +60,8 @@ struct mvg_comm {
 
 namespace {
 
+constexpr int kRing = 8;
+
 struct Shard {
     mvg_shard plan{};
     int device = 0;
@@ -71,11 +73,17 @@ struct Shard {
     int nsteps = 0;
     ncclComm_t xcomm[MVG_MAX_XSTEPS] = {};
     bool owns_xcomm[MVG_MAX_XSTEPS] = {};
-    hipStream_t stream = nullptr;
-    hipStream_t copy_stream = nullptr;
+    hipStream_t stream = nullptr;       // GEMV (and the root's distribution sends)
+    hipStream_t copy_stream = nullptr;  // H2D staging
+    hipStream_t xstream = nullptr;      // the exchange step (collectives), overlapping the next GEMV
     double* dA = nullptr;
     double* dx = nullptr;
-    double* dy_part = nullptr;  // local product: y_len (row/block) or R (col) doubles
+    // local product: y_len (row/block) or R (col) doubles; a ring of kRing buffers when an
+    // exchange follows: multiply n writes dy_parts[n % ring] while earlier exchanges still read
+    // the others
+    double* dy_parts[kRing] = {};
+    hipEvent_t gemv_done[kRing] = {};  // GEMV into dy_parts[b] finished
+    hipEvent_t x_done[kRing] = {};     // exchange reading dy_parts[b] finished
     double* dy_row = nullptr;   // block-split row leader: reduced slice (lr doubles)
     double* dy = nullptr;       // rank 0: the full y (R doubles)
     double* stage[2] = {nullptr, nullptr};  // root: staging for root->peer sends (rank mode)
@@ -94,6 +102,9 @@ struct mvg_engine {
     bool always_collect = false;  // run the collectives even at nranks == 1 (tests)
     bool distributed = false;
     int timing_every = 0;       // record kernel events on every Nth multiply (0 = off)
+    int64_t nx = 0;             // multiplies with an exchange issued so far
+    bool x_pending = false;     // an exchange may still run (slot (nx - 1) % ring)
+    int ring = kRing;           // ring length in use (MVG_XRING, 1 = exchange on the GEMV stream)
     int64_t multiply_calls = 0;
     double kernel_ms_sum = 0.0;
     int64_t kernel_launches = 0;
@@ -125,8 +136,14 @@ void free_shard(Shard& s) {
     (void)hipSetDevice(s.device);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.copy_stream) (void)hipStreamSynchronize(s.copy_stream);
-    for (double* p : {s.dA, s.dx, s.dy_part, s.dy_row, s.dy, s.stage[0], s.stage[1]})
+    if (s.xstream) (void)hipStreamSynchronize(s.xstream);
+    for (double* p : {s.dA, s.dx, s.dy_row, s.dy, s.stage[0], s.stage[1]})
         if (p) (void)hipFree(p);
+    for (int b = 0; b < kRing; ++b) {
+        if (s.dy_parts[b]) (void)hipFree(s.dy_parts[b]);
+        if (s.gemv_done[b]) (void)hipEventDestroy(s.gemv_done[b]);
+        if (s.x_done[b]) (void)hipEventDestroy(s.x_done[b]);
+    }
     for (auto& ev : s.ev_pool) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
@@ -136,6 +153,7 @@ void free_shard(Shard& s) {
         if (s.owns_xcomm[k] && s.xcomm[k]) (void)ncclCommDestroy(s.xcomm[k]);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.copy_stream) (void)hipStreamDestroy(s.copy_stream);
+    if (s.xstream) (void)hipStreamDestroy(s.xstream);
     s = Shard{};
 }
 
@@ -282,6 +300,8 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
     // forced collectives need an RCCL communicator (a one-device comm made without the
     // variable has none)
     e->always_collect = ac && ac[0] == '1' && comm->locals[0].comm != nullptr;
+    if (const char* v = getenv("MVG_XRING")) e->ring = std::max(1, std::min(kRing, atoi(v)));
+
     e->shards.resize(comm->locals.size());
     auto bail = [&](int code) {
         mvg_engine_destroy(e);
@@ -302,10 +322,24 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         if ((rc = alloc_doubles(&s.dA, p.n_rows * p.n_cols)) != MVG_OK) return bail(rc);
         if ((rc = alloc_doubles(&s.dx, x_len(p))) != MVG_OK) return bail(rc);
         const int64_t part = alg == MVG_ALG_COLWISE ? R : p.y_len;
-        if ((rc = alloc_doubles(&s.dy_part, part)) != MVG_OK) return bail(rc);
         if ((rc = mvg_plan_exchange(alg, R, C, comm->nranks, l.rank, e->always_collect, s.steps,
                                     MVG_MAX_XSTEPS, &s.nsteps)) != MVG_OK)
             return bail(rc);
+        if ((rc = alloc_doubles(&s.dy_parts[0], part)) != MVG_OK) return bail(rc);
+        if (s.nsteps > 0) {
+            for (int b = 1; b < e->ring; ++b)
+                if ((rc = alloc_doubles(&s.dy_parts[b], part)) != MVG_OK) return bail(rc);
+            if (hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking) != hipSuccess)
+                return bail(fail(MVG_E_HIP, "hipStreamCreate"));
+            for (int b = 0; b < e->ring; ++b)
+                // GEMV -> exchange kernel on the same device: no system-scope fence needed (the
+                // marker with one cost ~2 us of idle GPU per multiply); exchange -> collect's
+                // D2H copy keeps the default (host-visible) fence
+                if (hipEventCreateWithFlags(&s.gemv_done[b], hipEventDisableTiming | hipEventDisableSystemFence) !=
+                        hipSuccess ||
+                    hipEventCreateWithFlags(&s.x_done[b], hipEventDisableTiming) != hipSuccess)
+                    return bail(fail(MVG_E_HIP, "hipEventCreate"));
+        }
         bool need_row = false;
         for (int k = 0; k < s.nsteps; ++k)
             need_row |= s.steps[k].member && (s.steps[k].dst == MVG_X_BUF_ROW || s.steps[k].src == MVG_X_BUF_ROW);
@@ -393,6 +427,9 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
         // exactly one local shard
         Shard& s = e->shards[0];
         MVG_HIP(hipSetDevice(s.device));
+        // the sends/recvs below use the world communicator on s.stream: order them after any
+        // exchange still running on s.xstream (one communicator, one order of operations)
+        if (e->x_pending) MVG_HIP(hipStreamWaitEvent(s.stream, s.x_done[(e->nx - 1) % e->ring], 0));
         if (s.rank == 0) {
             const int64_t chunk_bytes = 256ll << 20;
             if (!s.stage[0]) {
@@ -492,11 +529,21 @@ int mvg_engine_multiply(mvg_engine* e) {
     const int nsteps = e->shards[0].nsteps;
     const bool solo = nsteps == 0;  // P == 1: the product goes straight into y
     const bool timed = e->timing_every > 0 && (e->multiply_calls++ % e->timing_every) == 0;
+    const bool serial = e->ring == 1;
+    const int b = solo ? 0 : (int)(e->nx % e->ring);
+    // The GEMV writes dy_parts[b]; the exchange that last read it was multiply nx - ring's. The
+    // GEMV stream waits once per ring, on the latest exchange (nx - 1): every slot is then free
+    // for the next `ring` GEMVs (the exchange stream runs in order), so one cross-stream wait is
+    // paid per ring instead of per multiply (measured: a wait per multiply cost more than the
+    // overlap saved at world size 1).
+    int wait_slot = -1;
+    if (!solo && !serial && e->x_pending && b == 0) wait_slot = (int)((e->nx - 1) % e->ring);
     // 1) local product on every device
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
         const mvg_shard& p = s.plan;
-        double* out = solo ? s.dy : s.dy_part;
+        if (wait_slot >= 0) MVG_HIP(hipStreamWaitEvent(s.stream, s.x_done[wait_slot], 0));
+        double* out = solo ? s.dy : s.dy_parts[b];
         hipEvent_t t0 = nullptr, t1 = nullptr;
         if (timed) {
             if (s.ev_used == s.ev_pool.size()) {
@@ -513,9 +560,15 @@ int mvg_engine_multiply(mvg_engine* e) {
         int rc = mvg_gemv(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream);
         if (rc != MVG_OK) return rc;
         if (timed) MVG_HIP(hipEventRecord(t1, s.stream));
+        if (!solo && !serial) {
+            MVG_HIP(hipEventRecord(s.gemv_done[b], s.stream));
+            MVG_HIP(hipStreamWaitEvent(s.xstream, s.gemv_done[b], 0));
+        }
     }
-    // 2) the exchange step, from the shared schedule (mvg_plan_exchange). A failing call inside
-    // the group still closes the group before the error is reported.
+    if (solo) return MVG_OK;
+    // 2) the exchange step, from the shared schedule (mvg_plan_exchange), on the exchange
+    // stream: it overlaps the next multiply's GEMV. A failing call inside the group still closes
+    // the group before the error is reported.
     for (int k = 0; k < nsteps; ++k) {
         MVG_NCCL(ncclGroupStart());
         ncclResult_t r = ncclSuccess;
@@ -524,15 +577,15 @@ int mvg_engine_multiply(mvg_engine* e) {
             const mvg_xstep& st = s.steps[k];
             if (!st.member) continue;
             (void)hipSetDevice(s.device);
-            double* bufs[3] = {s.dy_part, s.dy_row, s.dy};
+            double* bufs[3] = {s.dy_parts[b], s.dy_row, s.dy};
             const double* src = bufs[st.src];
             double* dst = bufs[st.dst];
-            if (!dst) dst = s.dy_part;  // recvbuff is only written on the root
+            if (!dst) dst = s.dy_parts[b];  // recvbuff is only written on the root
             if (st.op == MVG_X_GATHER) {
-                r = ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], s.stream);
+                r = ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
                 what = "ncclGather";
             } else {
-                r = ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], s.stream);
+                r = ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
                 what = "ncclReduce";
             }
             if (r != ncclSuccess) break;
@@ -541,6 +594,12 @@ int mvg_engine_multiply(mvg_engine* e) {
         if (r != ncclSuccess) return nccl_fail(r, what);
         if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
     }
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        if (!serial) MVG_HIP(hipEventRecord(s.x_done[b], s.xstream));
+    }
+    e->x_pending = !serial;
+    ++e->nx;
     return MVG_OK;
 }
 
@@ -551,7 +610,9 @@ int mvg_engine_sync(mvg_engine* e) {
         MVG_HIP(hipSetDevice(s.device));
         MVG_HIP(hipStreamSynchronize(s.copy_stream));
         MVG_HIP(hipStreamSynchronize(s.stream));
+        if (s.xstream) MVG_HIP(hipStreamSynchronize(s.xstream));
     }
+    e->x_pending = false;
     if (e->timing_every > 0) {
         // per timed multiply call: max over local devices, then summed
         size_t n = e->shards.empty() ? 0 : e->shards[0].ev_used;
@@ -587,6 +648,8 @@ int mvg_engine_collect(mvg_engine* e, double* y) {
         if (s.rank != 0) continue;
         if (!y) return fail(MVG_E_INVALID, "root needs a y buffer");
         MVG_HIP(hipSetDevice(s.device));
+        if (e->x_pending)  // y is complete once the last exchange is
+            MVG_HIP(hipStreamWaitEvent(s.stream, s.x_done[(e->nx - 1) % e->ring], 0));
         if (e->R > 0)
             MVG_HIP(hipMemcpyAsync(y, s.dy, (size_t)e->R * sizeof(double), hipMemcpyDeviceToHost, s.stream));
         MVG_HIP(hipStreamSynchronize(s.stream));

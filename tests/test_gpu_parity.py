@@ -147,6 +147,44 @@ def test_engine_forced_collectives_p1(alg, monkeypatch, golden):
         c.destroy()
 
 
+@pytest.mark.parametrize("ring", [1, 2, 8])
+@pytest.mark.parametrize("alg", ["rowwise", "colwise", "blockwise"])
+def test_engine_exchange_overlap_keeps_each_multiply_own_y(alg, ring, monkeypatch):
+    # The exchange of multiply i runs on its own stream beside the next multiplies' GEMVs, with
+    # the partial y in a ring of `ring` buffers (1: exchange on the GEMV stream). Changing x
+    # between back-to-back multiplies (no sync in between, across ring wrap-arounds) must still
+    # leave exactly the last multiply's y on the root, and a collect in between must see its own
+    # multiply's y.
+    monkeypatch.setenv("MVG_ALWAYS_COLLECT", "1")
+    monkeypatch.setenv("MVG_XRING", str(ring))
+    c = mm.Comm.init_all([0])
+    R, Cn = 2048, 4096
+    A = oracle.synth(R, Cn, 42)
+    xs = [oracle.synth(1, Cn, s)[0] for s in (11, 12, 13, 14)]
+    want = [oracle.multiply(alg, A, x, 1) for x in xs]
+    try:
+        with mm.Multiplier(alg, R, Cn, c) as e:
+            e.distribute(A, xs[0])
+            e.multiply()
+            assert max_rel(e.collect(), want[0]) <= TOL
+            for x in xs[1:]:
+                e.distribute(A, x)
+                e.multiply()
+                e.multiply()
+            assert max_rel(e.collect(), want[-1]) <= TOL
+            e.distribute(A, xs[1])
+            for _ in range(5):
+                e.multiply()
+            e.sync()
+            assert max_rel(e.collect(), want[1]) <= TOL
+            for i in range(19):
+                e.distribute(A, xs[i % 4])
+                e.multiply()
+            assert max_rel(e.collect(), want[18 % 4]) <= TOL
+    finally:
+        c.destroy()
+
+
 def test_engine_rank_mode_world_of_one(golden):
     uid = mm.Comm.unique_id()
     c = mm.Comm.init_rank(uid, 1, 0, 0)
