@@ -525,19 +525,25 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 //   8192 <= K < 16384    8 waves x 2 rows x 512-col chunks
 // Workgroups run in dispatch order: XCD-contiguous orders win <= 1.3 % on some shapes but lose
 // 5 % at 131072^2, where the 8 XCDs' streams land 2^34 B apart (variant_sweep11_xcd.jsonl).
-// Shorter rows:
-//   1536 < K < 8192   wave-owns-2-rows, pipelined + staggered start column
-//   768 < K <= 1536   wave-owns-4-rows, pipelined
+// Shorter rows (768 < K < 8192), by the size of A (variant_sweep14_grid.jsonl: 42 shapes
+// 1024..65536 x 1024..12288, the reference's test.sh squares among them):
+//   A < 1 GiB         row-per-workgroup again: 2 waves x 2 rows x 512-col chunks, or 8 waves for
+//                     6144 <= K with >= 700 workgroups (within 1.024x of the best variant on
+//                     average over those shapes, worst 1.08x; the wave-owns-rows forms below
+//                     were up to 1.57x slower there: 4200^2 29 -> 23.6 us, 1800^2 7.3 -> 5.5 us)
+//   A >= 1 GiB, 1536 < K    wave-owns-2-rows, pipelined + staggered start column
+//   A >= 1 GiB, K <= 1536   wave-owns-4-rows, pipelined
 //   K <= 768          one row per wave (the whole row is one chunk: 524288 short waves stream
 //                     consecutive memory, config 5's shard)
 static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) return K >= 256 ? 9 : 10;
+    const int64_t nrb = (M + 1) / 2;
     if (K >= 8192) {
-        const int64_t nrb = (M + 1) / 2;
         if (nrb < 700) return 48;
         return K >= 16384 ? 32 : 24;
     }
+    if (K > 768 && M * K < (int64_t)(1ll << 27)) return K >= 6144 && nrb >= 700 ? 24 : 33;
     if (K > 1536) return 15;
     if (K > 768) return 11;
     return 19;

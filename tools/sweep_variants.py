@@ -34,11 +34,21 @@ SHAPES = [
     ("mid_4096x32768", 4096, 32768),
     ("mid_1536x32768", 1536, 32768),
     ("cfg3_g1_65536sq", 65536, 65536),
+    ("ref_600sq", 600, 600),
+    ("ref_1800sq", 1800, 1800),
+    ("ref_4200sq", 4200, 4200),
+    ("ref_7800sq", 7800, 7800),
+    ("ref_10200sq", 10200, 10200),
 ]
 
 
 def main():
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+    if only:  # literal shapes "MxK" join the named ones
+        for n in only:
+            if "x" in n and n.replace("x", "").isdigit():
+                m, k = (int(v) for v in n.split("x"))
+                SHAPES.append((n, m, k))
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     max_elems = max(m * k for n, m, k in SHAPES if not only or n in only)
@@ -59,7 +69,12 @@ def main():
         nbytes = 8 * (M * K + K + M)
         results = {}
         prefixes = tuple(p.encode() for p in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["vec", "rowblk"]))
-        variants = [v for v in range(nvar) if lib.mvg_gemv_variant_name(v).startswith(prefixes)] + [0]
+        # a prefix ending in "$" names one variant exactly
+        exact = tuple(p[:-1] for p in prefixes if p.endswith(b"$"))
+        prefixes = tuple(p for p in prefixes if not p.endswith(b"$"))
+        variants = [v for v in range(nvar)
+                    if (prefixes and lib.mvg_gemv_variant_name(v).startswith(prefixes))
+                    or lib.mvg_gemv_variant_name(v) in exact] + [0]
         y = torch.empty(M, dtype=torch.float64, device=dev)
         for v in variants:
             y.zero_()
