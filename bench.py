@@ -91,7 +91,10 @@ def main():
     if world != n:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run")
     torch.cuda.set_device(local)
-    distributed = world > 1
+    # MVG_BENCH_FORCE_DIST=1 runs the one-process-per-GPU path (process group, RCCL comm from the
+    # group, shared-memory distribution, root sends) even at world size 1, to rehearse it on a
+    # one-GPU box
+    distributed = world > 1 or os.environ.get("MVG_BENCH_FORCE_DIST") == "1"
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
