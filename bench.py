@@ -12,9 +12,10 @@ is the max over ranks; value = algorithmic bytes of all ranks / that time.
 
 Also reported: `roofline` (the GEMV kernel alone: bytes per launch / its mean duration from
 HIP events on the engine stream; peak 8 TB/s; `traffic` from the committed rocprofv3 PMC
-summary when one matches this configuration), `cpu_baseline` (rank 0 at N = 1: the oracle's
-restatement of the reference's MPI loop timed on this host's cores, reference timing
-semantics), and `end_to_end` (distribution from the root's host memory + multiply + y on
+summary when one matches this configuration), `cpu_baseline` (rank 0 at N = 1: the real
+reference, oracle/_ref under mpiexec, on a sample of the same matrix, with the oracle's
+restatement of its MPI loop on the full matrix beside it; the restatement alone when the
+reference cannot run), and `end_to_end` (distribution from the root's host memory + multiply + y on
 the root, the reference's timing semantics).
 """
 from __future__ import annotations
@@ -52,6 +53,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-sample-bytes", type=float, default=2.2e9,
                     help="CPU baseline runs on the leading rows of the same matrix up to this size")
+    ap.add_argument("--no-ref-baseline", action="store_true",
+                    help="time only the oracle port, not the real reference (oracle/_ref)")
+    ap.add_argument("--ref-rows", type=int, default=1024,
+                    help="rows of the sample the real reference runs on (its loop is 100 iterations)")
+    ap.add_argument("--ref-timeout", type=float, default=240.0)
     return ap.parse_args()
 
 
@@ -270,7 +276,46 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
 
 
 def cpu_baseline(args, R, C, y_gpu):
-    """The reference's CPU path (oracle restatement, P threads as MPI ranks, distribution
+    """The reference's CPU path timed on this host. Preferred: the real reference (oracle/_ref,
+    built from its own sources, run with MPICH's mpiexec on P = the port's thread count) on the
+    leading --ref-rows rows of the same matrix, kind "reference"; its 100-iteration loop is fixed
+    in its source. Always also: the oracle port (below), reported under "port" (or as the
+    baseline itself, kind "port", when the reference cannot run here)."""
+    port = cpu_port_baseline(args, R, C, y_gpu)
+    if args.no_ref_baseline:
+        return port
+    from oracle import ref_runner
+
+    P = port["cores"]
+    rows = min(R, args.ref_rows)
+    if args.alg in ("rowwise", "blockwise"):
+        from oracle import oracle
+
+        gr = P if args.alg == "rowwise" else oracle.grid_shape(P)[0]
+        rows = max(gr, rows - rows % gr)
+    if not ref_runner.available(args.alg) or not _splits(args.alg, rows, C, P):
+        port["reference"] = "not run: oracle/_ref or mpiexec absent, or the sample does not split"
+        return port
+    try:
+        r = ref_runner.run(args.alg, rows, C, P, timeout=args.ref_timeout)
+    except Exception as exc:  # the baseline must never sink the bench
+        port["reference"] = f"not run: {str(exc)[:300]}"
+        return port
+    rel = float(np.max(np.abs(y_gpu[:rows] - r["y"]) / np.abs(r["y"])))
+    assert rel <= 1e-12, f"GPU y differs from the reference's own y: {rel}"
+    nbytes = 8 * (rows * C + C + rows)
+    return {"value": round(nbytes / r["seconds"] / 1e9, 3), "unit": "GB/s", "cores": P, "kind": "reference",
+            "ms_per_step": round(r["seconds"] * 1e3, 3), "iters": 100,
+            "sample": f"leading {rows} of {R} rows ({rows}x{C}) {args.alg}: the reference's own executable "
+                      f"(oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its text inputs, its "
+                      f"100-iteration loop (distribution from the root + sequential sums + collection); "
+                      f"run {r['wall_s']:.1f} s incl. text loading; GPU y matches its y to {rel:.1e}",
+            "host_cpu": host_cpu(),
+            "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")}}
+
+
+def cpu_port_baseline(args, R, C, y_gpu):
+    """The oracle restatement of the reference's CPU path (P threads as MPI ranks, distribution
     from the root's A included, mean of per-iteration max) on this host, on the full workload
     or, above --cpu-sample-bytes, on its leading rows (same values, same algorithm)."""
     from oracle import oracle

@@ -1,0 +1,70 @@
+"""Runs the REAL reference (oracle/_ref/multiplier_<alg>, built by oracle/build_ref.sh from the
+reference's own sources) under MPICH's mpiexec — TEST INFRASTRUCTURE ONLY.
+
+Used by bench.py's cpu_baseline leg (kind "reference") to time the reference's CPU path on the
+GPU box's host cores, and available to tests. The reference reads ./data/matrix_R_C.txt and
+./data/vector_C.txt relative to its working directory (matr_utils.c:10,16,45,68), times its own
+100-iteration loop (multiplier_rowwise.c:135-151, colwise.c:218-233, blockwise.c:361-378) and
+appends "R, C, P, time" to ./data/out/<alg>.csv (rowwise.c:160-169); oracle/ref_dump.h makes rank
+0 dump y to $ORACLE_Y. Inputs are the synthetic values in the reference's own "%.4f" text form
+(include/matvec_gpu.h spec), so y is directly comparable with the GPU's y on the same rows.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import tempfile
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_BIN = os.path.join(HERE, "_ref")
+MPIEXEC = os.environ.get("MVG_MPIEXEC", "/opt/conda/bin/mpiexec")
+
+
+def available(alg: str) -> bool:
+    return os.access(os.path.join(REF_BIN, f"multiplier_{alg}"), os.X_OK) and os.access(MPIEXEC, os.X_OK)
+
+
+def write_inputs(data_dir: str, R: int, C: int, seed_a: int = 42, seed_x: int = 4242) -> None:
+    """The synthetic A and x as the reference's text files (values k/10000, "%.4f")."""
+    from matvec_mpi_multiplier_amd._lib import check, lib
+
+    check(lib.mvg_write_matr_synth(os.path.join(data_dir, f"matrix_{R}_{C}.txt").encode(), R, C, seed_a),
+          "mvg_write_matr_synth")
+    check(lib.mvg_write_matr_synth(os.path.join(data_dir, f"vector_{C}.txt").encode(), 1, C, seed_x),
+          "mvg_write_matr_synth")
+
+
+def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str | None = None) -> dict:
+    """mpiexec -n P multiplier_<alg> R C in a scratch directory. Returns {"seconds": mean time
+    per iteration as the reference printed it, "y": rank 0's y, "wall_s": whole run incl. text
+    loading}. Raises RuntimeError on any failure."""
+    if not available(alg):
+        raise RuntimeError(f"reference executable or {MPIEXEC} missing")
+    own = workdir is None
+    work = workdir or tempfile.mkdtemp(prefix="mvg_ref_")
+    try:
+        data = os.path.join(work, "data")
+        os.makedirs(os.path.join(data, "out"), exist_ok=True)
+        write_inputs(data, R, C)
+        csv = os.path.join(data, "out", f"{alg}.csv")
+        if os.path.exists(csv):
+            os.remove(csv)
+        ypath = os.path.join(work, "y.txt")
+        env = dict(os.environ, ORACLE_Y=ypath)
+        cmd = [MPIEXEC, "-n", str(P), os.path.join(REF_BIN, f"multiplier_{alg}"), str(R), str(C)]
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=timeout)
+        wall = time.perf_counter() - t0
+        if r.returncode != 0 or not os.path.exists(csv) or not os.path.exists(ypath):
+            raise RuntimeError(f"reference {alg} P={P} failed (rc {r.returncode}): {r.stdout[-400:]} {r.stderr[-400:]}")
+        last = [ln for ln in open(csv).read().splitlines() if ln.strip()][-1]
+        seconds = float(last.split(",")[3])
+        y = np.loadtxt(ypath, dtype=np.float64, ndmin=1)
+        return {"seconds": seconds, "y": y, "wall_s": wall}
+    finally:
+        if own:
+            shutil.rmtree(work, ignore_errors=True)

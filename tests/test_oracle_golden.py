@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN_DIR, case_inputs, golden_runs, max_rel
-from oracle import oracle
+from oracle import oracle, ref_runner
 
 
 def _runs():
@@ -90,3 +90,20 @@ def test_oracle_timing_harness_returns_reference_y():
         t, y = oracle.time_multiply(alg, A, x, 4, 3)
         assert t > 0
         np.testing.assert_array_equal(y, oracle.multiply(alg, A, x, 4))
+
+
+@pytest.mark.skipif(not all(ref_runner.available(a) for a in ("rowwise", "colwise", "blockwise")),
+                    reason="oracle/_ref (the reference built from its sources) or mpiexec absent")
+def test_ref_runner_real_reference_matches_oracle():
+    # bench.py's cpu_baseline leg runs the real reference through this runner on the GPU box;
+    # its y must be the oracle's (bit for bit for row split; col/block: MPI reduction order)
+    R, C, P = 32, 256, 4
+    A, x = oracle.synth(R, C, 42), oracle.synth(1, C, 4242)[0]
+    for alg in ("rowwise", "colwise", "blockwise"):
+        r = ref_runner.run(alg, R, C, P, timeout=120)
+        assert r["seconds"] > 0
+        want = oracle.multiply(alg, A, x, P)
+        if alg == "rowwise":
+            np.testing.assert_array_equal(r["y"], want)
+        else:
+            np.testing.assert_allclose(r["y"], want, rtol=1e-15)
