@@ -15,6 +15,7 @@
 //                      include/matvec_gpu.h) on the host — the large configs have no files
 //   MVG_Y_OUT=path     write y, "%.17g" per line (the reference never writes y)
 //   MVG_DATA_DIR=dir   input directory (default ./data, matr_utils.c:45,68)
+//   MVG_ITER_LOG=path  write every timed iteration's end-to-end time (s), one per line
 // Besides the CSV it prints the device-resident time (GEMV + collective only, A resident).
 #include <errno.h>
 #include <stdint.h>
@@ -155,6 +156,10 @@ int main(int argc, char** argv) {
     }
     // pinned host memory: distribution runs at full PCIe rate on every GPU's own link
     const bool pinned = nA > 0 && mvg_host_register(A.data(), nA * sizeof(double)) == MVG_OK;
+    // x and y too: a pageable 600-element y cost 22 us per collect against 13 us page-locked
+    // (tools/e2e_small.py)
+    const bool pinned_x = mvg_host_register(x.data(), x.size() * sizeof(double)) == MVG_OK;
+    const bool pinned_y = mvg_host_register(y.data(), y.size() * sizeof(double)) == MVG_OK;
 
     std::vector<int> devs(comm_sz);
     for (int i = 0; i < comm_sz; ++i) devs[i] = i;
@@ -165,6 +170,8 @@ int main(int argc, char** argv) {
 
     // the reference's timed loop (rowwise.c:135-151): distribution included, root holds y
     double sum_time = 0.0;
+    std::vector<double> it_times;
+    it_times.reserve((size_t)iters);
     for (long it = 0; it < iters; ++it) {
         if ((rc = mvg_engine_sync(eng)) != MVG_OK) return die(rc, "sync");
         const double t0 = now_s();
@@ -172,7 +179,8 @@ int main(int argc, char** argv) {
         if ((rc = mvg_engine_multiply(eng)) != MVG_OK) return die(rc, "multiply");
         if ((rc = mvg_engine_collect(eng, y.data())) != MVG_OK) return die(rc, "collect");
         if ((rc = mvg_engine_sync(eng)) != MVG_OK) return die(rc, "sync");  // MPI_Barrier
-        sum_time += now_s() - t0;
+        it_times.push_back(now_s() - t0);
+        sum_time += it_times.back();
     }
     // device-resident: A already on the GPUs; GEMV + exchange only
     mvg_engine_kernel_timing(eng, 5);  // events on every 5th multiply (each pair costs ~6 us)
@@ -186,15 +194,23 @@ int main(int argc, char** argv) {
     mvg_engine_kernel_ms(eng, &kms, &nk);
     const double bytes = 8.0 * ((double)nA + (double)n_cols * (alg == MVG_ALG_ROWWISE ? comm_sz : 1) + (double)n_rows);
     printf("end-to-end (distribute + multiply + y on root): mean %.6f s over %ld iterations\n", sum_time / iters, iters);
-    printf("device-resident: %.3f ms per multiply, %.1f GB/s aggregate; GEMV kernel %.3f ms (max over GPUs)\n",
+    printf("device-resident: %.4f ms per multiply, %.1f GB/s aggregate; GEMV kernel %.3f ms (max over GPUs)\n",
            dev_s * 1e3, bytes / dev_s / 1e9, kms);
 
+    if (const char* tl = getenv("MVG_ITER_LOG")) {  // per-iteration end-to-end times, seconds
+        if (FILE* f = fopen(tl, "w")) {
+            for (double t : it_times) fprintf(f, "%.9f\n", t);
+            fclose(f);
+        }
+    }
     if (const char* yo = getenv("MVG_Y_OUT")) {
         if ((rc = mvg_write_vec(yo, y.data(), n_rows)) != MVG_OK) return die(rc, "mvg_write_vec");
     }
     mvg_engine_destroy(eng);
     mvg_comm_destroy(comm);
     if (pinned) mvg_host_unregister(A.data());
+    if (pinned_x) mvg_host_unregister(x.data());
+    if (pinned_y) mvg_host_unregister(y.data());
 
     FILE* fp = fopen(csv, "a");  // rowwise.c:160-169
     if (!fp) {

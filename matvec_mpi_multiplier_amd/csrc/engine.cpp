@@ -347,6 +347,45 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
             if ((rc = alloc_doubles(&s.dy_row, p.y_len)) != MVG_OK) return bail(rc);
         if (l.rank == 0)
             if ((rc = alloc_doubles(&s.dy, R)) != MVG_OK) return bail(rc);
+        // Warm the device before any timed loop: first-touch every buffer (the first H2D into
+        // never-touched HBM ran at 11 GB/s instead of 56, tools/numa_h2d.py) and launch the
+        // shard's GEMV once (loads its code object and any split-K workspace). These one-time
+        // costs are the GPU runtime's analogue of MPI_Init; without this they landed in the
+        // executables' first timed iteration (+0.1 ms on the mean at 600 x 600).
+        auto zero = [&](double* p, int64_t n) {
+            return p && n > 0 ? hipMemsetAsync(p, 0, (size_t)n * sizeof(double), s.stream) : hipSuccess;
+        };
+        hipError_t ze = zero(s.dA, p.n_rows * p.n_cols);
+        if (ze == hipSuccess) ze = zero(s.dx, x_len(p));
+        for (int b = 0; b < kRing && ze == hipSuccess; ++b) ze = zero(s.dy_parts[b], part);
+        if (ze == hipSuccess) ze = zero(s.dy_row, p.y_len);
+        if (ze == hipSuccess) ze = zero(s.dy, R);
+        if (ze != hipSuccess) return bail(hip_fail(ze, "hipMemsetAsync"));
+        if ((rc = mvg_gemv(s.dA, p.n_cols, s.dx, s.dy_parts[0], p.n_rows, p.n_cols, s.stream)) != MVG_OK)
+            return bail(rc);
+        // ... and one page-locked H2D into A's buffer and D2H out of y's, as large as those
+        // transfers will be up to 4 MiB, on each stream that distributes or collects. The
+        // runtime brings its large-copy path up on the first such transfer of the process:
+        // 8.2 ms once (tools/first_copy.py: 2.88 MB from any page-locked buffer, 8.2 ms first,
+        // 66 us after; 512-B copies do not trigger it), which otherwise landed in the
+        // executables' first timed iteration (bin/multiplier_rowwise 600 600, MVG_ITER_LOG).
+        const int64_t a_elems = std::min<int64_t>(p.n_rows * p.n_cols, 1 << 19);
+        const int64_t y_elems = std::min<int64_t>(part, 1 << 19);
+        const size_t wbytes = (size_t)std::max<int64_t>({a_elems, y_elems, 1}) * sizeof(double);
+        double* pinned = nullptr;
+        if (hipHostMalloc((void**)&pinned, wbytes, hipHostMallocDefault) != hipSuccess)
+            return bail(fail(MVG_E_NOMEM, "hipHostMalloc (engine warm-up)"));
+        memset(pinned, 0, wbytes);
+        hipError_t we = hipSuccess;
+        for (hipStream_t st : {s.stream, s.copy_stream}) {
+            if (we == hipSuccess && a_elems > 0)
+                we = hipMemcpyAsync(s.dA, pinned, (size_t)a_elems * sizeof(double), hipMemcpyHostToDevice, st);
+            if (we == hipSuccess && y_elems > 0)
+                we = hipMemcpyAsync(pinned, s.dy_parts[0], (size_t)y_elems * sizeof(double), hipMemcpyDeviceToHost, st);
+            if (we == hipSuccess) we = hipStreamSynchronize(st);
+        }
+        (void)hipHostFree(pinned);
+        if (we != hipSuccess) return bail(hip_fail(we, "engine warm-up"));
     }
     // Sub-communicators of the exchange schedule. ncclCommSplit is collective over the world,
     // so every local rank calls it for every split step, inside one group per step.
