@@ -18,9 +18,23 @@ HDRS     := $(CSRC)/common.h include/matvec_gpu.h
 OBJS     := $(BUILD)/gemv.o $(BUILD)/host.o $(BUILD)/engine.o $(BUILD)/textio.o
 APPS     := bin/multiplier_rowwise bin/multiplier_colwise bin/multiplier_blockwise
 
+# The executables' launcher (apps/launch.h): over MPI when one is installed (the image's MPICH
+# under /opt/conda, or MPI_HOME=...), so `mpiexec -n P bin/multiplier_<alg>` runs P ranks; else
+# single-process only. MPI stays inside bin/libmvg_launch.so and its own run path.
+MPI_HOME ?= /opt/conda
+ifneq ($(wildcard $(MPI_HOME)/include/mpi.h),)
+LAUNCH_SRC  := apps/launch_mpi.c
+LAUNCH_LIBS := -I$(MPI_HOME)/include -L$(MPI_HOME)/lib -lmpi -Wl,-rpath,$(MPI_HOME)/lib
+else
+LAUNCH_SRC  := apps/launch_none.c
+LAUNCH_LIBS :=
+endif
+LAUNCH   := bin/libmvg_launch.so
+APP_LINK := -L$(PKG) -lmatvec_gpu -Lbin -lmvg_launch -Wl,-rpath,'$$ORIGIN/../$(PKG)' -Wl,-rpath,'$$ORIGIN' -lpthread
+
 EXAMPLES := bin/rowwise_binding
 
-all: $(LIB) $(APPS) $(EXAMPLES) oracle
+all: $(LIB) $(LAUNCH) $(APPS) $(EXAMPLES) oracle
 
 examples: $(EXAMPLES)
 
@@ -40,18 +54,22 @@ $(BUILD)/%.o: $(CSRC)/%.cpp $(HDRS) | $(BUILD)
 $(LIB): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJS) -o $@ $(LDLIBS)
 
-bin/multiplier_rowwise: apps/multiplier_main.cpp $(LIB) include/matvec_gpu.h | $(BUILD)
-	g++ -O2 -std=c++17 -Wall -DMVG_APP_ALG=0 $< -o $@ -L$(PKG) -lmatvec_gpu -Wl,-rpath,'$$ORIGIN/../$(PKG)' -lpthread
-bin/multiplier_colwise: apps/multiplier_main.cpp $(LIB) include/matvec_gpu.h | $(BUILD)
-	g++ -O2 -std=c++17 -Wall -DMVG_APP_ALG=1 $< -o $@ -L$(PKG) -lmatvec_gpu -Wl,-rpath,'$$ORIGIN/../$(PKG)' -lpthread
-bin/multiplier_blockwise: apps/multiplier_main.cpp $(LIB) include/matvec_gpu.h | $(BUILD)
-	g++ -O2 -std=c++17 -Wall -DMVG_APP_ALG=2 $< -o $@ -L$(PKG) -lmatvec_gpu -Wl,-rpath,'$$ORIGIN/../$(PKG)' -lpthread
+$(LAUNCH): $(LAUNCH_SRC) apps/launch.h | $(BUILD)
+	gcc -O2 -std=c99 -fPIC -shared -Wall -Wextra $(LAUNCH_SRC) -o $@ $(LAUNCH_LIBS)
+
+APP_DEPS := apps/multiplier_main.cpp apps/launch.h $(LIB) $(LAUNCH) include/matvec_gpu.h
+bin/multiplier_rowwise: $(APP_DEPS) | $(BUILD)
+	g++ -O2 -std=c++17 -Wall -DMVG_APP_ALG=0 $< -o $@ $(APP_LINK)
+bin/multiplier_colwise: $(APP_DEPS) | $(BUILD)
+	g++ -O2 -std=c++17 -Wall -DMVG_APP_ALG=1 $< -o $@ $(APP_LINK)
+bin/multiplier_blockwise: $(APP_DEPS) | $(BUILD)
+	g++ -O2 -std=c++17 -Wall -DMVG_APP_ALG=2 $< -o $@ $(APP_LINK)
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APPS) $(EXAMPLES)
+	rm -rf $(BUILD) $(LIB) $(LAUNCH) $(APPS) $(EXAMPLES)
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle examples

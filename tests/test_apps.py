@@ -98,3 +98,68 @@ def test_c_binding_example_runs_the_fixture(workdir, golden):
     y = np.array([float(v) for v in r.stdout.split()[-4:]])
     assert max_rel(y, golden["fixture_4x8/rowwise/P1"]) <= 1e-12
     assert re.fullmatch(r"4, 8, 1, \d+\.\d{6}\n", r.stderr.splitlines()[-1] + "\n")
+
+
+# ---- launched like the reference: mpiexec -n P bin/multiplier_<alg> R C (test.sh:11)
+MPIEXEC = "/opt/conda/bin/mpiexec"
+needs_mpiexec = pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no MPI launcher in this image")
+
+
+def mpirun(alg, np_, args, cwd, **env):
+    e = dict(os.environ, **{k: str(v) for k, v in env.items()})
+    return subprocess.run([MPIEXEC, "-n", str(np_), os.path.join(REPO, "bin", f"multiplier_{alg}")]
+                          + [str(a) for a in args], cwd=cwd, env=e, capture_output=True, text=True, timeout=300)
+
+
+@needs_mpiexec
+@pytest.mark.parametrize("alg,R,C,P,msg", [
+    ("rowwise", 4, 8, 3, "4 mod 3 = 1. Unable to parallellize task."),
+    ("colwise", 4, 8, 3, "8 mod 3 = 2. Unable to parallellize task."),
+    ("blockwise", 5, 5, 2, "25 mod 2 = 1. Unable to parallellize task."),
+])
+def test_mpiexec_indivisible_root_prints_every_rank_exits_zero(workdir, alg, R, C, P, msg):
+    # P comes from the launcher, as in the reference; only the root prints, and unlike the
+    # reference (whose other ranks are left waiting in MPI_Barrier) every rank exits 0
+    r = mpirun(alg, P, [R, C], workdir)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("ERROR!!!") == 1 and msg in r.stdout
+
+
+@needs_mpiexec
+def test_mpiexec_missing_input_every_rank_exits_zero(workdir):
+    r = mpirun("rowwise", 2, [6, 6], workdir)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("Unable to locate matrix file 'matrix_6_6.txt'") == 1
+    assert "comm_sz = 2\nmy_rank = 0\n" in r.stdout  # the banner reports the launcher's P
+    assert (workdir / "data" / "out" / "rowwise.csv").read_text() == "n_rows, n_cols, n_processes, time\n"
+
+
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("dist", ["shared", "send"])
+@pytest.mark.parametrize("alg", ALGS)
+def test_mpiexec_rank_mode_fixture_matches_reference(workdir, golden, alg, dist):
+    # the one-GPU-per-rank path (MPI bootstrap, RCCL communicator from the broadcast unique id,
+    # shared-window or root-send distribution, max-over-ranks timing) at P = 1, collectives forced
+    yout = workdir / "y.txt"
+    env = dict(MVG_RANK_MODE=1, MVG_ALWAYS_COLLECT=1, MVG_ITERS=5, MVG_Y_OUT=yout)
+    if dist == "send":
+        env["MVG_DIST"] = "send"
+    r = mpirun(alg, 1, [4, 8], workdir, **env)
+    assert r.returncode == 0, r.stderr
+    assert "launch: 1 ranks, one GPU each" in r.stdout
+    assert ("shared window" in r.stdout) == (dist == "shared")
+    assert max_rel(np.loadtxt(yout), golden[f"fixture_4x8/{alg}/P1"]) <= 1e-12
+    lines = (workdir / "data" / "out" / f"{alg}.csv").read_text().splitlines()
+    assert re.fullmatch(r"4, 8, 1, \d+\.\d{6}", lines[1]), lines
+
+
+@needs_mpiexec
+@pytest.mark.gpu
+def test_mpiexec_more_ranks_than_gpus_fails_cleanly(workdir):
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    r = mpirun("rowwise", n, [4 * n, 8], workdir, MVG_SYNTH=1, MVG_ITERS=1)
+    assert r.returncode != 0
+    assert f"{n} GPU(s) needed on this node" in r.stderr
