@@ -5,8 +5,10 @@
 //
 // The reference parses with one fscanf per value; at 16384^2 and up (1.9-120 GB of text)
 // that is impractical, so here the file is mmap'd, split into per-thread ranges on
-// whitespace boundaries, tokens are counted, prefix-summed, then parsed with strtod (the
-// conversion fscanf("%lf") performs), so the doubles are bit-identical to the reference's.
+// whitespace boundaries, tokens are counted, prefix-summed, then converted exactly as strtod
+// (the conversion fscanf("%lf") performs) would: Clinger's exact fast path for short decimal
+// tokens (parse_fast), strtod itself for the rest, so the doubles are bit-identical to the
+// reference's.
 // Differences, all deliberate: 64-bit indices; a file with fewer tokens than R*C is an error
 // (the reference ignores fscanf's return and leaves garbage); the file is closed.
 #include <errno.h>
@@ -29,6 +31,71 @@ namespace {
 
 inline bool is_space(char c) {
     return c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
+}
+
+constexpr double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                               1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Decimal token -> double without strtod for the common case, Clinger's fast path: a token
+// [+-]digits[.digits][(e|E)[+-]digits] whose significant digits (leading and trailing zeros
+// dropped) form an integer m <= 2^53 and whose decimal exponent e lies in [-22, 22]. Then m and
+// 10^|e| are exact doubles and one IEEE multiply or divide rounds the exact value once, to
+// nearest — the double strtod (correctly rounded) returns. The reference's inputs ("%.4f",
+// README.md:32) always take this path; anything else (more digits, hex, inf/nan, a malformed
+// token) returns false and the caller falls back to strtod, so results never differ from it.
+inline bool parse_fast(const char* p, const char* end, double* out) {
+    bool neg = false;
+    if (p < end && (*p == '+' || *p == '-')) neg = *p++ == '-';
+    uint64_t m = 0;
+    int nd = 0;     // digits in m (from the first nonzero digit on)
+    int zeros = 0;  // zeros seen since the last nonzero digit, not yet folded into m
+    int e10 = 0;
+    bool any = false, dot = false;
+    for (; p < end; ++p) {
+        const char c = *p;
+        if (c >= '0' && c <= '9') {
+            any = true;
+            if (dot) --e10;
+            if (c == '0') {
+                if (nd) ++zeros;
+                continue;
+            }
+            for (; zeros > 0; --zeros, ++nd) {
+                if (nd >= 19) return false;
+                m *= 10;
+            }
+            if (nd >= 19) return false;
+            m = m * 10 + (uint64_t)(c - '0');
+            ++nd;
+        } else if (c == '.' && !dot) {
+            dot = true;
+        } else {
+            break;
+        }
+    }
+    if (!any) return false;
+    e10 += zeros;  // trailing zeros: m * 10^zeros
+    if (p < end) {
+        if (*p != 'e' && *p != 'E') return false;
+        ++p;
+        bool eneg = false;
+        if (p < end && (*p == '+' || *p == '-')) eneg = *p++ == '-';
+        if (p >= end) return false;
+        int ex = 0;
+        for (; p < end; ++p) {
+            if (*p < '0' || *p > '9') return false;
+            if (ex < 100000) ex = ex * 10 + (*p - '0');
+        }
+        e10 += eneg ? -ex : ex;
+    }
+    if (m == 0) {
+        *out = neg ? -0.0 : 0.0;
+        return true;
+    }
+    if (m > (1ull << 53) || e10 < -22 || e10 > 22) return false;
+    const double v = e10 < 0 ? (double)m / kPow10[-e10] : (double)m * kPow10[e10];
+    *out = neg ? -v : v;
+    return true;
 }
 
 // Parse the first n tokens of the file into out. Returns MVG_OK / MVG_E_IO.
@@ -109,7 +176,9 @@ int parse_file(const std::string& path, int64_t n, double* out) {
                     size_t j = i;
                     while (j < end && !is_space(base[j])) ++j;
                     const size_t tl = j - i;
-                    if (tl < sizeof(buf)) {
+                    if (parse_fast(base + i, base + j, &out[k])) {
+                        // exact: the value strtod would return
+                    } else if (tl < sizeof(buf)) {
                         memcpy(buf, base + i, tl);
                         buf[tl] = '\0';
                         char* ep = nullptr;

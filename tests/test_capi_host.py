@@ -225,6 +225,29 @@ def test_synth_text_roundtrip_parallel_parser(tmp_path):
     np.testing.assert_array_equal(A, np.loadtxt(tmp_path / f"matrix_{R}_{Cn}.txt"))
 
 
+def test_parser_is_bit_identical_to_strtod(tmp_path):
+    # the loader's exact fast path (Clinger: short decimal tokens) and its strtod fallback must
+    # give the double strtod/fscanf("%lf") gives for every token; Python's float() is correctly
+    # rounded, as glibc's strtod is
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([rng.uniform(-1e6, 1e6, 3000), rng.uniform(0, 1, 3000),
+                           rng.standard_normal(2000) * 10.0 ** rng.integers(-30, 30, 2000)])
+    toks = [f"{v:.4f}" for v in vals[:6000]]                      # the reference's format
+    toks += [f"{v:.17g}" for v in vals] + [f"{v:.18e}" for v in vals[::3]] + [f"{v:.6g}" for v in vals[::2]]
+    toks += [str(int(v)) for v in vals[:500]] + [f"{v:.2f}E+3" for v in vals[:300]]
+    toks += ["0", "-0", "-0.0", "+5", ".5", "5.", "-.25", "1e22", "1e23", "1e-22", "1e-23", "22e-22",
+             "9007199254740992", "9007199254740993", "9007199254740993e-5", "0.000000000000000000000001",
+             "123456789012345678901234567890", "1234567890123456789", "12345678901234567890e-30",
+             "1E5", "4.9e-324", "1.7976931348623157e308", "2.2250738585072014e-308", "1e400", "-1e-400",
+             "0.10000000000000000555", "100000000000000000000000", "3.0000000000000000000000001",
+             "inf", "-inf", "Infinity", "0x1.8p1", "00000000000000000000000012.5000000000000000000000"]
+    (tmp_path / f"vector_{len(toks)}.txt").write_text("\n".join(toks) + "\n")
+    got = mm.load_vec(len(toks), str(tmp_path))
+    want = np.array([float.fromhex(t) if t.startswith("0x") else float(t) for t in toks])
+    bad = [t for t, g, w in zip(toks, got.view(np.uint64), want.view(np.uint64)) if g != w]
+    assert not bad, bad[:10]
+
+
 def test_write_vec_roundtrips(tmp_path):
     v = np.array([222.19999999999999, 1e-300, -0.0, 3.141592653589793, 1076.4842229100022])
     mm.write_vec(str(tmp_path / "vector_5.txt"), v)
