@@ -158,6 +158,11 @@ const char* mvg_gemv_variant_name(int variant);
  * of nv products approaches that of one. Same numerics contract as mvg_gemv. */
 int mvg_gemv_multi(const double* d_A, int64_t lda, const double* d_X, int64_t ldx, double* d_Y,
                    int64_t ldy, int64_t m, int64_t k, int nv, void* stream);
+/* mvg_gemv_multi with an explicit kernel variant (0 = automatic; tests and sweeps) */
+int mvg_gemv_multi_variant(const double* d_A, int64_t lda, const double* d_X, int64_t ldx, double* d_Y,
+                           int64_t ldy, int64_t m, int64_t k, int nv, int variant, void* stream);
+int mvg_gemv_multi_variant_count(void);
+const char* mvg_gemv_multi_variant_name(int variant);
 
 /* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */
 int mvg_stream_read(const double* d_src, int64_t n, double* d_sink, void* stream);

@@ -103,6 +103,9 @@ SIGNATURES = {
     "mvg_gemv_variant_name": (C.c_char_p, [C.c_int]),
     "mvg_gemv_auto_variant": (C.c_int, [_i64, _i64, _i64]),
     "mvg_gemv_multi": (C.c_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, C.c_int, _p]),
+    "mvg_gemv_multi_variant": (C.c_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, C.c_int, C.c_int, _p]),
+    "mvg_gemv_multi_variant_count": (C.c_int, []),
+    "mvg_gemv_multi_variant_name": (C.c_char_p, [C.c_int]),
     "mvg_stream_read": (C.c_int, [_p, _i64, _p, _p]),
     "mvg_comm_unique_id": (C.c_int, [C.c_char_p]),
     "mvg_comm_init_all": (C.c_int, [C.POINTER(_p), C.c_int, C.POINTER(C.c_int)]),

@@ -616,15 +616,133 @@ static int launch(int v, const double* A, int64_t lda, const double* x, double* 
 }
 
 // ------------------------------------------------------------------ several x per pass
-// Y[:, v] = A X[:, v] for v < nv (nv <= NV): the row-per-workgroup stream of A with NV x
-// vectors consumed per A chunk, so A is read once for all of them. X and Y
-// are column-major (vector v at X + v*ldx, Y + v*ldy). Vectors v >= nv alias vector 0 and are
-// never stored. Per-wave sums meet in LDS and are added in wave order (deterministic).
-template <int NW, int RPB, int UNR, int NV>
-__global__ __launch_bounds__(NW * 64) void gemv_multi(const double* __restrict__ A, int64_t lda,
-                                                      const double* __restrict__ X, int64_t ldx,
-                                                      double* __restrict__ Y, int64_t ldy, int64_t M,
-                                                      int64_t K, int nv) {
+// Y[:, v] = A X[:, v] for v < nv: A is streamed once for NV vectors. X and Y
+// are column-major (vector v at X + v*ldx, Y + v*ldy); vectors v >= nv alias vector 0 and are
+// never stored. Per lane: the A pairs of its rows and the x pairs of all NV vectors for the same
+// columns, FMAs in a fixed order, then fixed-order reductions (deterministic). The x reads
+// (NV per A read shared by the rows of a lane) are L2 hits: A's HBM stream is the roofline.
+template <int RPG, int NV, int UNR>
+__device__ __forceinline__ void mload(const double* const (&arow)[RPG], const double* const (&xv)[NV],
+                                      int64_t base, int64_t step, dbl2 (&xa)[NV][UNR], dbl2 (&aa)[RPG][UNR]) {
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) aa[r][u] = load2<true>(arow[r] + base + u * step);
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) xa[v][u] = load2<false>(xv[v] + base + u * step);
+}
+
+template <int RPG, int NV, int UNR>
+__device__ __forceinline__ void mfma(double (&acc)[RPG][NV], const dbl2 (&xa)[NV][UNR], const dbl2 (&aa)[RPG][UNR]) {
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                acc[r][v] = __builtin_fma(aa[r][u].x, xa[v][u].x, acc[r][v]);
+                acc[r][v] = __builtin_fma(aa[r][u].y, xa[v][u].y, acc[r][v]);
+            }
+}
+
+template <int RPG, int NV>
+__device__ __forceinline__ void mtail(double (&acc)[RPG][NV], const double* const (&arow)[RPG],
+                                      const double* const (&xv)[NV], int64_t c, int64_t K) {
+    if (c + 1 < K) {
+        dbl2 xx[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xx[v] = load2<false>(xv[v] + c);
+#pragma unroll
+        for (int r = 0; r < RPG; ++r) {
+            const dbl2 a = load2<true>(arow[r] + c);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                acc[r][v] = __builtin_fma(a.x, xx[v].x, acc[r][v]);
+                acc[r][v] = __builtin_fma(a.y, xx[v].y, acc[r][v]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < RPG; ++r)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) acc[r][v] = __builtin_fma(arow[r][c], xv[v][c], acc[r][v]);
+    }
+}
+
+// Wave-group form (short and mid rows): a wave64 is split into 64/LPR groups of LPR lanes; each
+// group owns RPG rows and walks them left to right, UNR 16-B pairs per lane per chunk, chunk
+// i+1's loads issued before chunk i's FMAs. The groups of a wave read the same x addresses (one
+// fetch per wave instruction), so x costs NV/(RPG*64/LPR) of A's cache-line traffic.
+template <int LPR, int RPG, int NV, int UNR>
+__global__ __launch_bounds__(kBlock) void gemv_mvec(const double* __restrict__ A, int64_t lda,
+                                                    const double* __restrict__ X, int64_t ldx,
+                                                    double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                    int64_t K, int nv) {
+    constexpr int G = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR;
+    const int gl = lane % LPR;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t row0 = (wave * G + g) * RPG;
+    const double* arow[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    const double* xv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xv[v] = X + (v < nv ? v : 0) * ldx;
+    double acc[RPG][NV];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[r][v] = 0.0;
+
+    constexpr int64_t kStep = 2 * LPR;
+    constexpr int64_t kChunk = kStep * UNR;
+    const int64_t nch = K / kChunk;
+    const int64_t c0 = 2 * gl;
+    if (nch > 0) {
+        dbl2 xa[NV][UNR], xb[NV][UNR];
+        dbl2 aa[RPG][UNR], ab[RPG][UNR];
+        mload<RPG, NV, UNR>(arow, xv, c0, kStep, xa, aa);
+        int64_t i = 1;
+        for (; i + 1 < nch; i += 2) {
+            mload<RPG, NV, UNR>(arow, xv, i * kChunk + c0, kStep, xb, ab);
+            mfma<RPG, NV, UNR>(acc, xa, aa);
+            mload<RPG, NV, UNR>(arow, xv, (i + 1) * kChunk + c0, kStep, xa, aa);
+            mfma<RPG, NV, UNR>(acc, xb, ab);
+        }
+        if (i < nch) {
+            mload<RPG, NV, UNR>(arow, xv, i * kChunk + c0, kStep, xb, ab);
+            mfma<RPG, NV, UNR>(acc, xa, aa);
+            mfma<RPG, NV, UNR>(acc, xb, ab);
+        } else {
+            mfma<RPG, NV, UNR>(acc, xa, aa);
+        }
+    }
+    for (int64_t c = nch * kChunk + c0; c < K; c += kStep) mtail<RPG, NV>(acc, arow, xv, c, K);
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const double s = group_sum<LPR>(acc[r][v]);
+            if (gl == 0 && row0 + r < M && v < nv) Y[v * ldy + row0 + r] = s;
+        }
+}
+
+// Workgroup form (long rows): workgroup b (NW waves) owns rows [b*RPB, +RPB); wave w takes
+// column chunks w, w+NW, ... of them (the single-vector gemv_rowblock stream), pipelined; the
+// per-wave sums meet in LDS and are added in wave order.
+template <int NW, int RPB, int NV, int UNR>
+__global__ __launch_bounds__(NW * 64) void gemv_mrow(const double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ X, int64_t ldx,
+                                                     double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                     int64_t K, int nv) {
     __shared__ double part[NW][RPB][NV];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -649,46 +767,27 @@ __global__ __launch_bounds__(NW * 64) void gemv_multi(const double* __restrict__
     constexpr int64_t kChunk = kStep * UNR;
     const int64_t nch = K / kChunk;
     const int64_t c0 = 2 * lane;
-    for (int64_t i = w; i < nch; i += NW) {
-        const int64_t base = i * kChunk + c0;
-        dbl2 a[RPB][UNR];
-#pragma unroll
-        for (int r = 0; r < RPB; ++r)
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) a[r][u] = load2<true>(arow[r] + base + u * kStep);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            dbl2 xx[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) xx[u] = load2<false>(xv[v] + base + u * kStep);
-#pragma unroll
-            for (int r = 0; r < RPB; ++r)
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    acc[r][v] = __builtin_fma(a[r][u].x, xx[u].x, acc[r][v]);
-                    acc[r][v] = __builtin_fma(a[r][u].y, xx[u].y, acc[r][v]);
-                }
-        }
-    }
-    for (int64_t c = nch * kChunk + 2 * (int64_t)threadIdx.x; c < K; c += 2 * NW * 64) {
-        if (c + 1 < K) {
-#pragma unroll
-            for (int r = 0; r < RPB; ++r) {
-                const dbl2 a = load2<true>(arow[r] + c);
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const dbl2 xx = load2<false>(xv[v] + c);
-                    acc[r][v] = __builtin_fma(a.x, xx.x, acc[r][v]);
-                    acc[r][v] = __builtin_fma(a.y, xx.y, acc[r][v]);
-                }
+    int64_t i = w;
+    if (i < nch) {
+        dbl2 xa[NV][UNR], xb[NV][UNR];
+        dbl2 aa[RPB][UNR], ab[RPB][UNR];
+        mload<RPB, NV, UNR>(arow, xv, i * kChunk + c0, kStep, xa, aa);
+        for (; i + NW < nch; i += 2 * NW) {
+            mload<RPB, NV, UNR>(arow, xv, (i + NW) * kChunk + c0, kStep, xb, ab);
+            mfma<RPB, NV, UNR>(acc, xa, aa);
+            if (i + 2 * NW < nch) {
+                mload<RPB, NV, UNR>(arow, xv, (i + 2 * NW) * kChunk + c0, kStep, xa, aa);
+                mfma<RPB, NV, UNR>(acc, xb, ab);
+            } else {
+                mfma<RPB, NV, UNR>(acc, xb, ab);
+                i = nch;
+                break;
             }
-        } else {
-#pragma unroll
-            for (int r = 0; r < RPB; ++r)
-#pragma unroll
-                for (int v = 0; v < NV; ++v) acc[r][v] = __builtin_fma(arow[r][c], xv[v][c], acc[r][v]);
         }
+        if (i < nch) mfma<RPB, NV, UNR>(acc, xa, aa);
     }
+    for (int64_t c = nch * kChunk + 2 * (int64_t)threadIdx.x; c < K; c += 2 * NW * 64)
+        mtail<RPB, NV>(acc, arow, xv, c, K);
 #pragma unroll
     for (int r = 0; r < RPB; ++r)
 #pragma unroll
@@ -706,6 +805,60 @@ __global__ __launch_bounds__(NW * 64) void gemv_multi(const double* __restrict__
             Y[v * ldy + row0 + r] = s;
         }
     }
+}
+
+typedef void (*gemv_multi_fn)(const double*, int64_t, const double*, int64_t, double*, int64_t, int64_t,
+                              int64_t, int);
+
+struct MultiVariant {
+    const char* name;
+    gemv_multi_fn fn[3];  // NV = 2, 4, 8
+    int rows_per_block;
+    int block;
+};
+
+#define MVEC(LPR, RPG, UNR)                                                                              \
+    {"mvec_l" #LPR "_r" #RPG "_u" #UNR,                                                                  \
+     {gemv_mvec<LPR, RPG, 2, UNR>, gemv_mvec<LPR, RPG, 4, UNR>, gemv_mvec<LPR, RPG, 8, UNR>},            \
+     (kBlock / 64) * (64 / LPR) * RPG, kBlock}
+#define MROW(NW, RPB, UNR)                                                                               \
+    {"mrow_w" #NW "_r" #RPB "_u" #UNR,                                                                   \
+     {gemv_mrow<NW, RPB, 2, UNR>, gemv_mrow<NW, RPB, 4, UNR>, gemv_mrow<NW, RPB, 8, UNR>}, RPB, NW * 64}
+
+static const MultiVariant kMultiVariants[] = {
+    {"auto", {nullptr, nullptr, nullptr}, 0, 0},  // 0
+    MVEC(16, 1, 1),                               // 1
+    MVEC(16, 2, 1),                               // 2
+    MVEC(16, 1, 2),                               // 3
+    MVEC(32, 1, 1),                               // 4
+    MVEC(32, 2, 1),                               // 5
+    MVEC(64, 1, 1),                               // 6
+    MVEC(64, 2, 1),                               // 7
+    MVEC(64, 1, 2),                               // 8
+    MROW(4, 2, 1),                                // 9
+    MROW(4, 2, 2),                                // 10
+    MROW(4, 4, 1),                                // 11
+    MROW(8, 2, 1),                                // 12
+    MROW(8, 1, 2),                                // 13
+    MROW(4, 1, 2),                                // 14
+    MVEC(16, 4, 1),                               // 15
+    MVEC(32, 4, 1),                               // 16
+    MVEC(64, 4, 1),                               // 17
+    MVEC(16, 3, 1),                               // 18
+    MVEC(32, 3, 1),                               // 19
+    MROW(4, 8, 1),                                // 20
+    MROW(2, 4, 1),                                // 21
+};
+constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVariants[0]));
+
+// From the MI355X sweeps (tools/multi_bench.py -> profiles/r01/multi_sweep.jsonl; 8 shapes, K = 512
+// ... 65536): per (nv group, K class) the variant with the best geometric mean, within 1.01-1.07x
+// of the best variant per shape (worst 1.17x).
+int pick_multi_variant(int64_t m, int64_t k, int nvp) {
+    (void)m;
+    if (nvp <= 2) return k <= 1024 ? 5 : 11;   // mvec_l32_r2_u1 | mrow_w4_r4_u1
+    if (nvp <= 4) return k <= 1024 ? 18 : 21;  // mvec_l16_r3_u1 | mrow_w2_r4_u1
+    return k <= 1024 ? 15 : 16;                // mvec_l16_r4_u1 | mvec_l32_r4_u1
 }
 
 // ------------------------------------------------------------------ other kernels
@@ -793,39 +946,58 @@ int mvg_gemv(const double* A, int64_t lda, const double* x, double* y, int64_t m
     return mvg_gemv_variant(A, lda, x, y, m, k, 0, stream);
 }
 
-int mvg_gemv_multi(const double* A, int64_t lda, const double* X, int64_t ldx, double* Y, int64_t ldy,
-                   int64_t m, int64_t k, int nv, void* stream) {
+int mvg_gemv_multi_variant_count(void) { return kNumMultiVariants; }
+
+const char* mvg_gemv_multi_variant_name(int v) {
+    if (v < 0 || v >= kNumMultiVariants) return "invalid";
+    return kMultiVariants[v].name;
+}
+
+int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_t ldx, double* Y,
+                           int64_t ldy, int64_t m, int64_t k, int nv, int variant, void* stream) {
     if (m < 0 || k < 0 || nv < 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: negative size");
+    if (variant < 0 || variant >= kNumMultiVariants) return fail(MVG_E_INVALID, "mvg_gemv_multi: bad variant");
     if (m == 0 || nv == 0) return MVG_OK;
-    if (!A || !X || !Y || lda < k || ldx < k || ldy < m)
+    if (!Y || ldy < m || (k > 0 && (!A || !X || lda < k || ldx < k)))
         return fail(MVG_E_INVALID, "mvg_gemv_multi: null pointer or leading dimension too small");
     hipStream_t s = (hipStream_t)stream;
     const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)X % 16 == 0) && lda % 2 == 0 && ldx % 2 == 0;
-    if (!vec || k == 0) {  // the 8-B path: one vector at a time
+    if (!vec || k == 0) {  // the 8-B path (or k = 0): one vector at a time
+        if (variant != 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: variants need even lda/ldx, 16-B aligned A, X");
         for (int v = 0; v < nv; ++v) {
             int rc = mvg_gemv_variant(A, lda, X + v * ldx, Y + v * ldy, m, k, vec ? 0 : 9, stream);
             if (rc != MVG_OK) return rc;
         }
         return MVG_OK;
     }
-    constexpr int NW = 8, RPB = 2;
-    const int64_t blocks = (m + RPB - 1) / RPB;
-    if (blocks > (1ll << 31) / (NW * 64)) return fail(MVG_E_INVALID, "mvg_gemv_multi: too many rows");
     for (int v0 = 0; v0 < nv; v0 += 8) {  // groups of <= 8 vectors per pass over A
         const int g = nv - v0 < 8 ? nv - v0 : 8;
         const double* Xg = X + v0 * ldx;
         double* Yg = Y + v0 * ldy;
-        if (g == 1)
-            hipLaunchKernelGGL((gemv_multi<NW, RPB, 4, 1>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
-        else if (g == 2)
-            hipLaunchKernelGGL((gemv_multi<NW, RPB, 4, 2>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
-        else if (g <= 4)
-            hipLaunchKernelGGL((gemv_multi<NW, RPB, 2, 4>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
-        else
-            hipLaunchKernelGGL((gemv_multi<NW, RPB, 2, 8>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, A, lda, Xg, ldx, Yg, ldy, m, k, g);
-        MVG_HIP(hipGetLastError());
+        if (g == 1 && variant == 0) {  // one vector: the single-vector dispatch
+            int rc = mvg_gemv_variant(A, lda, Xg, Yg, m, k, 0, stream);
+            if (rc != MVG_OK) return rc;
+            continue;
+        }
+        const int slot = g <= 2 ? 0 : g <= 4 ? 1 : 2;
+        const int v = variant ? variant : pick_multi_variant(m, k, 2 << slot);
+        const MultiVariant& mv = kMultiVariants[v];
+        // launches of < 2^32 threads each (the grid-size cap), row ranges in order
+        const int64_t max_rows = ((1ll << 31) / mv.block) * mv.rows_per_block;
+        for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
+            const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
+            const int64_t blocks = (mm + mv.rows_per_block - 1) / mv.rows_per_block;
+            hipLaunchKernelGGL(mv.fn[slot], dim3((unsigned)blocks), dim3(mv.block), 0, s, A + r0 * lda, lda, Xg,
+                               ldx, Yg + r0, ldy, mm, k, g);
+            MVG_HIP(hipGetLastError());
+        }
     }
     return MVG_OK;
+}
+
+int mvg_gemv_multi(const double* A, int64_t lda, const double* X, int64_t ldx, double* Y, int64_t ldy,
+                   int64_t m, int64_t k, int nv, void* stream) {
+    return mvg_gemv_multi_variant(A, lda, X, ldx, Y, ldy, m, k, nv, 0, stream);
 }
 
 int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {

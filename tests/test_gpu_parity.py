@@ -328,6 +328,34 @@ def test_multi_vector_gemv(m, k, nv):
         assert max_rel(Y[:, v], oracle.multiply_std_rowwise(A, np.ascontiguousarray(X[:, v]))) <= TOL, v
 
 
+@pytest.mark.parametrize("m,k,nv", [(257, 1000, 2), (130, 4226, 4), (33, 6002, 8), (1000, 512, 3), (77, 256, 8),
+                                    (9, 130, 5), (4099, 64, 2)])
+def test_multi_vector_every_variant(m, k, nv):
+    """Every mvg_gemv_multi kernel variant, with row and column tails (rows not a multiple of a
+    block's rows, K not a multiple of a chunk), against the oracle per vector; columns of Y past
+    nv are never written."""
+    from matvec_mpi_multiplier_amd._lib import check, lib
+
+    A = oracle.synth(m, k, 42)
+    X = oracle.synth(nv, k, 4242)  # nv x k: vector v contiguous (column-major k x nv)
+    want = [oracle.multiply_std_rowwise(A, np.ascontiguousarray(X[v])) for v in range(nv)]
+    dA, dX = mm.DeviceBuffer(m * k).upload(A), mm.DeviceBuffer(nv * k).upload(X)
+    dY = mm.DeviceBuffer(m * 8)
+    try:
+        for var in range(1, lib.mvg_gemv_multi_variant_count()):
+            name = lib.mvg_gemv_multi_variant_name(var).decode()
+            dY.upload(np.full(m * 8, np.nan))
+            check(lib.mvg_gemv_multi_variant(dA.ptr, k, dX.ptr, k, dY.ptr, m, m, k, nv, var, None), name)
+            check(lib.mvg_stream_sync(None), "sync")
+            Y = dY.download(m * 8).reshape(8, m)
+            for v in range(nv):
+                assert max_rel(Y[v], want[v]) <= TOL, (name, v)
+            assert np.isnan(Y[nv:]).all(), name
+    finally:
+        for b in (dA, dX, dY):
+            b.free()
+
+
 def test_distribute_shared_from_dev_shm(comm1, golden, tmp_path):
     """bench.py's N > 1 'shared' end-to-end path at world size 1: A in a /dev/shm segment,
     pinned with hipHostRegister, pulled by the GPU, y vs the reference's golden y."""
