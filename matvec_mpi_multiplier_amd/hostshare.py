@@ -49,7 +49,13 @@ class SharedHostMatrix:
         name = f"mvg_{tag}"
         me = None
         if dist.get_rank() == 0:
-            shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
+            try:
+                shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
+            except FileExistsError:  # left behind by a killed run with the same tag: replace it
+                stale = shared_memory.SharedMemory(name=name)
+                stale.close()
+                stale.unlink()
+                shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
             me = cls(shm, (R, C), owner=True)
             if R * C:
                 check(lib.mvg_synth_fill_host(me.array.ctypes.data, C, R, C, 0, 0, C, seed), "mvg_synth_fill_host")

@@ -155,9 +155,13 @@ def _shm_worker(rank, world, port, R, C, outq):
         dist.destroy_process_group()
 
 
-def test_shared_host_matrix_two_ranks():
+@pytest.mark.parametrize("stale", [False, True])
+def test_shared_host_matrix_two_ranks(stale):
     """bench.py's end-to-end `shared` distribution: rank 0 creates the root's A in /dev/shm,
-    rank 1 maps the same bytes, both unmap, the segment is removed (no leak)."""
+    rank 1 maps the same bytes, both unmap, the segment is removed (no leak). A segment of the
+    same name left by a killed run is replaced, not fatal."""
+    from multiprocessing import resource_tracker, shared_memory
+
     from matvec_mpi_multiplier_amd.hostshare import shm_free_bytes
 
     if shm_free_bytes() < (64 << 20):
@@ -165,6 +169,10 @@ def test_shared_host_matrix_two_ranks():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    if stale:
+        old = shared_memory.SharedMemory(name=f"mvg_test_{port}", create=True, size=4096)
+        resource_tracker.unregister(old._name, "shared_memory")  # left behind on purpose
+        old.close()
     procs = [ctx.Process(target=_shm_worker, args=(r, 2, port, 96, 80, q)) for r in range(2)]
     for p in procs:
         p.start()
