@@ -427,6 +427,7 @@ typedef void (*gemv_fn)(const double*, int64_t, const double*, double*, int64_t,
 typedef void (*gemv_split_fn)(const double*, int64_t, const double*, double*, int64_t, int64_t,
                               int64_t, int64_t);
 
+
 struct Variant {
     const char* name;
     gemv_fn fn;
