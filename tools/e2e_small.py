@@ -34,7 +34,7 @@ def main():
     from matvec_mpi_multiplier_amd._lib import lib, check
 
     comm = mm.Comm.init_all([0])
-    for n in (600, 1800, 4200):
+    for n in (600, 1200, 1800, 3000, 4200):
         eng = mm.Multiplier(args.alg, n, n, comm)
         A = mm.synth_host(n, n, 42)
         x = mm.synth_host(1, n, 4242)[0].copy()
@@ -66,7 +66,7 @@ def main():
             if it >= 10:
                 for k, dt in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t5 - t4)):
                     ph[k].append(dt * 1e6)
-        out = {"alg": args.alg, "n": n, "spin": args.spin, "pin_xy": args.pin_xy,
+        out = {"alg": args.alg, "n": n, "spin": args.spin, "pin_xy": args.pin_xy, "h2d_split": os.environ.get("MVG_H2D_SPLIT", "0"),
                "A_h2d_GBps_median": round(A.nbytes / (np.median(ph["distribute"]) * 1e-6) / 1e9, 1)}
         for k, v in ph.items():
             out[k + "_us_median"] = round(float(np.median(v)), 1)
