@@ -66,7 +66,7 @@ def main():
             if it >= 10:
                 for k, dt in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t5 - t4)):
                     ph[k].append(dt * 1e6)
-        out = {"alg": args.alg, "n": n, "spin": args.spin, "pin_xy": args.pin_xy, "h2d_split": os.environ.get("MVG_H2D_SPLIT", "0"),
+        out = {"alg": args.alg, "n": n, "spin": args.spin, "pin_xy": args.pin_xy, 
                "A_h2d_GBps_median": round(A.nbytes / (np.median(ph["distribute"]) * 1e-6) / 1e9, 1)}
         for k, v in ph.items():
             out[k + "_us_median"] = round(float(np.median(v)), 1)
