@@ -18,6 +18,7 @@
 //   MVG_NGPUS=G        GPUs to use in the single-process mode (default: all visible)
 //   MVG_DIST=send      rank mode: root-send distribution instead of the shared window
 //   MVG_RANK_MODE=1    rank-mode code path even for P = 1 (tests; with MVG_MPI=1 no mpiexec)
+//   MVG_SAME_DEVICE=1  rank mode with every rank on GPU 0 (tests on a one-GPU machine)
 //   MVG_ITERS=n        timed iterations (default 100, as the reference's loop, rowwise.c:135)
 //   MVG_SYNTH=1        skip the text files and generate the synthetic inputs (spec in
 //                      include/matvec_gpu.h) on the host — the large configs have no files
@@ -93,6 +94,18 @@ int main(int argc, char** argv) {
     // $MVG_NGPUS, else every visible device (only then is the GPU runtime touched before the
     // divisibility check, as MPI_Init precedes it in the reference).
     const bool ranks = L.mpi && (L.size > 1 || env_long("MVG_RANK_MODE", 0) == 1);
+    // MVG_SAME_DEVICE=1 (tests on a one-GPU machine): every rank uses GPU 0. RCCL refuses two
+    // ranks on one device of one host, so each rank names its own host (NCCL_HOSTID) and the
+    // ranks talk over loopback sockets — slow, but the multi-rank path runs end to end.
+    const bool same_dev = ranks && env_long("MVG_SAME_DEVICE", 0) == 1;
+    if (same_dev) {
+        char hid[64];
+        snprintf(hid, sizeof hid, "mvg-rank-%d", L.rank);
+        setenv("NCCL_HOSTID", hid, 0);
+        setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+        setenv("NCCL_IB_DISABLE", "1", 0);
+    }
+    const int my_device = same_dev ? 0 : L.local_rank;
     int comm_sz = L.mpi ? L.size : (int)env_long("MVG_NGPUS", 0);
     int ndev = 0;
     if (comm_sz <= 0) {
@@ -213,7 +226,7 @@ int main(int argc, char** argv) {
 
     // devices: rank mode takes the node-local rank's GPU; the single process takes 0..G-1
     rc = mvg_device_count(&ndev);
-    const int need = ranks ? L.local_rank + 1 : comm_sz;
+    const int need = ranks ? my_device + 1 : comm_sz;
     if (launch_all_min(rc == MVG_OK && need <= ndev ? 1 : 0) == 0) {
         if (root || rc != MVG_OK || need > ndev)
             fprintf(stderr, "rank %d: %d GPU(s) needed on this node, %d visible: %s\n", L.rank,
@@ -237,13 +250,13 @@ int main(int argc, char** argv) {
 
     mvg_comm* comm = nullptr;
     if (ranks) {
-        if ((rc = mvg_set_device(L.local_rank)) != MVG_OK) return fatal(rc, "mvg_set_device");
+        if ((rc = mvg_set_device(my_device)) != MVG_OK) return fatal(rc, "mvg_set_device");
         unsigned char uid[MVG_UNIQUE_ID_BYTES] = {0};
         int ok = 1;
         if (root && (rc = mvg_comm_unique_id(uid)) != MVG_OK) ok = die(rc, "mvg_comm_unique_id", L.rank) == 0;
         if (launch_all_min(ok) == 0) return finish(1);
         launch_bcast(uid, sizeof uid, 0);
-        rc = mvg_comm_init_rank(&comm, uid, comm_sz, L.rank, L.local_rank);
+        rc = mvg_comm_init_rank(&comm, uid, comm_sz, L.rank, my_device);
     } else {
         std::vector<int> devs(comm_sz);
         for (int i = 0; i < comm_sz; ++i) devs[i] = i;

@@ -96,6 +96,14 @@ def main():
     n = args.gpus
     if world != n:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run")
+    # MVG_SAME_DEVICE=1 (rehearsal on a one-GPU machine): every rank on GPU 0; RCCL refuses two
+    # ranks on one device of one host, so each rank names its own host and the ranks talk over
+    # loopback sockets (timings then mean nothing; the N > 1 code path runs end to end)
+    if os.environ.get("MVG_SAME_DEVICE") == "1" and world > 1:
+        os.environ.setdefault("NCCL_HOSTID", f"mvg-rank-{rank}")
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        local = 0
     torch.cuda.set_device(local)
     # MVG_BENCH_FORCE_DIST=1 runs the one-process-per-GPU path (process group, RCCL comm from the
     # group, shared-memory distribution, root sends) even at world size 1, to rehearse it on a

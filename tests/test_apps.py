@@ -4,6 +4,7 @@ import os
 import re
 import shutil
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -163,3 +164,48 @@ def test_mpiexec_more_ranks_than_gpus_fails_cleanly(workdir):
     r = mpirun("rowwise", n, [4 * n, 8], workdir, MVG_SYNTH=1, MVG_ITERS=1)
     assert r.returncode != 0
     assert f"{n} GPU(s) needed on this node" in r.stderr
+
+
+# ---- more than one rank on a one-GPU machine: every rank on GPU 0 (MVG_SAME_DEVICE=1), RCCL
+# over loopback sockets. The multi-rank code path (MPI bootstrap, shared-window and root-send
+# distribution, ncclGather / ncclReduce / ncclCommSplit + two-level exchange) against the real
+# reference's own y for the same P.
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,P,dist", [("rowwise", 2, "shared"), ("rowwise", 4, "send"), ("colwise", 3, "shared"),
+                                        ("colwise", 4, "send"), ("blockwise", 4, "shared"), ("blockwise", 3, "send")])
+def test_mpiexec_multi_rank_matches_reference(tmp_path, golden, alg, P, dist):
+    (tmp_path / "data" / "out").mkdir(parents=True)
+    yout = tmp_path / "y.txt"
+    env = dict(MVG_SYNTH=1, MVG_SAME_DEVICE=1, MVG_ITERS=3, MVG_Y_OUT=yout)
+    if dist == "send":
+        env["MVG_DIST"] = "send"
+    r = mpirun(alg, P, [480, 480], tmp_path, **env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert f"launch: {P} ranks" in r.stdout
+    assert max_rel(np.loadtxt(yout), golden[f"sq_480/{alg}/P{P}"]) <= 1e-12
+    lines = (tmp_path / "data" / "out" / f"{alg}.csv").read_text().splitlines()
+    assert re.fullmatch(rf"480, 480, {P}, \d+\.\d{{6}}", lines[1]), lines
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_device(tmp_path):
+    """bench.py's N > 1 path (the driver's scaling runs) at N = 2 under torch.distributed.run,
+    both ranks on GPU 0: one JSON line, whole-job bytes, end-to-end y equal to the device y."""
+    import json
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MVG_SAME_DEVICE="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--e2e-iters", "1"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["R"] == 32768 and d["config"]["bytes_per_step"] == 2 * 2147745792
+    assert "mean_s" in d["end_to_end"]["root_send"]  # shared may be skipped when /dev/shm is small
