@@ -15,8 +15,10 @@ HIP events on the engine stream; peak 8 TB/s; `traffic` from the committed rocpr
 summary when one matches this configuration), `cpu_baseline` (rank 0 at N = 1: the real
 reference, oracle/_ref under mpiexec, on a sample of the same matrix, with the oracle's
 restatement of its MPI loop on the full matrix beside it; the restatement alone when the
-reference cannot run), and `end_to_end` (distribution from the root's host memory + multiply + y on
-the root, the reference's timing semantics).
+reference cannot run), `end_to_end` (distribution from the root's host memory + multiply + y on
+the root, the reference's timing semantics), and `configs`: BASELINE.json configs 3-5 at their
+own fixed sizes on the same N GPUs (strong scaling, device-resident, same engine, same step),
+so one scaling run covers every multi-GPU config; supplementary, never `value`.
 """
 from __future__ import annotations
 
@@ -58,6 +60,8 @@ def parse():
     ap.add_argument("--ref-rows", type=int, default=1024,
                     help="rows of the sample the real reference runs on (its loop is 100 iterations)")
     ap.add_argument("--ref-timeout", type=float, default=240.0)
+    ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs 3-5 section")
+    ap.add_argument("--config-steps", type=int, default=20)
     return ap.parse_args()
 
 
@@ -167,6 +171,13 @@ def main():
     if not args.no_e2e and args.e2e_iters > 0:
         e2e = end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y, total_bytes, local)
 
+    # ---- BASELINE configs 3-5 at their own sizes on these N GPUs (the main engine's HBM is
+    # released first: config 4 is 128 GiB per GPU at N = 1)
+    configs = None
+    if not args.no_configs:
+        eng.destroy()
+        configs = baseline_configs(args, mm, comm, n, rank, local, distributed, barrier)
+
     # ---- CPU baseline: rank 0 at N = 1 only
     cpu = None
     if rank == 0 and n == 1 and not args.no_cpu_baseline:
@@ -188,7 +199,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text inputs)",
             "config": {
-                "workload": f"config 2 weak-scaled: {args.alg} of a ({R} x {C}) fp64 matrix, "
+                "workload": ("config 2 weak-scaled: " if (args.rows, args.cols) == (None, SHARD) else "")
+                            + f"{args.alg} of a ({R} x {C}) fp64 matrix, "
                             f"{sh.n_rows} x {sh.n_cols} shard per GPU, device-resident",
                 "alg": args.alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
                 "parallelism": f"{args.alg} over {n} GPU(s), exchange "
@@ -209,6 +221,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "configs": configs,
         }
         json_out.write(json.dumps(out) + "\n")
         json_out.flush()
@@ -217,6 +230,76 @@ def main():
     comm.destroy()
     if distributed:
         dist.destroy_process_group()
+
+
+# BASELINE.json configs[2..4], each at its own fixed size (strong scaling over N)
+BASELINE_CONFIGS = [
+    ("config 3", "colwise", 65536, 65536),
+    ("config 4", "blockwise", 131072, 131072),
+    ("config 5", "rowwise", 4194304, 512),
+]
+
+
+def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
+    """Configs 3-5 of BASELINE.json on the same N GPUs: device-resident synthetic inputs, one step
+    = GEMV on every shard + the algorithm's RCCL exchange (col: ncclReduce of R doubles; block:
+    row-communicator ncclReduce + leaders' ncclGather on the utils.c:26-37 grid, 2 x 4 at N = 8;
+    row: ncclGather), --config-steps steps timed between barriers, max over ranks. A config
+    whose shard does not fit in free HBM on every rank is skipped on all of them (the decision
+    is all-reduced so no rank waits in a collective another skipped)."""
+    import torch
+    import torch.distributed as dist
+
+    out = []
+    for name, alg, R, C in BASELINE_CONFIGS:
+        sh = mm.plan_shard(alg, R, C, n, rank)
+        part = R if alg == "colwise" else sh.y_len
+        need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + 9 * part + R) + (1 << 30)
+        free = torch.cuda.mem_get_info(local)[0]
+        ok = torch.tensor([1.0 if free >= need else 0.0], dtype=torch.float64, device=f"cuda:{local}")
+        if distributed:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if float(ok[0]) < 1.0:
+            out.append({"config": name, "alg": alg, "R": R, "C": C, "skipped": f"needs {need >> 30} GiB of HBM per GPU"})
+            continue
+        e = mm.Multiplier(alg, R, C, comm)
+        try:
+            e.fill_synth()
+            for _ in range(3):
+                e.multiply()
+            e.sync()
+            e.kernel_timing(args.event_every)
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.config_steps):
+                e.multiply()
+            e.sync()
+            barrier()
+            el = time.perf_counter() - t0
+            kt = e.kernel_ms()
+            e.kernel_timing(0)
+            t = torch.tensor([el, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
+            if distributed:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, kms = float(t[0]), float(t[1])
+            y = e.collect()
+            if rank == 0:
+                assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range"
+        finally:
+            e.destroy()
+        total = sum(8 * (s.n_rows * s.n_cols + s.n_cols + (R if alg == "colwise" else s.y_len))
+                    for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
+        per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
+        gr, gc = mm.get_2_most_closest_multipliers(n)
+        out.append({
+            "config": name, "alg": alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
+            "grid": [gr, gc] if alg == "blockwise" else None,
+            "value": round(total * args.config_steps / el / 1e9, 1), "unit": "GB/s",
+            "ms_per_step": round(el / args.config_steps * 1e3, 4), "steps": args.config_steps,
+            "kernel": kernel_name(sh), "kernel_ms": round(kms, 5),
+            "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
+        })
+    return out
 
 
 def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_bytes, local):
