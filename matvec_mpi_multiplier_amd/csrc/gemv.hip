@@ -808,6 +808,121 @@ __global__ __launch_bounds__(NW * 64) void gemv_mrow(const double* __restrict__ 
     }
 }
 
+// LDS form (mid and long rows, nv >= 2): the mvec/mrow forms hold every vector's x pairs in
+// registers next to A's, double-buffered, which leaves room for only 4-8 KiB of A in flight per
+// wave at nv = 8. Here the 4 waves of a workgroup (RPW rows each) walk the same column chunks
+// (128 * UNR columns) in lockstep; the chunk's x for all NV vectors is loaded once per workgroup
+// (one dbl2 of it per thread per 256), parked in a double-buffered LDS tile, and read back by
+// every wave with conflict-free ds_read_b128 right before its FMAs. Registers go to A: chunk
+// i + 1's A and x loads are issued before chunk i's FMAs; one barrier per chunk. The column tail
+// (K % chunk) reads x from global; per-lane FMAs in a fixed order, fixed-order reductions.
+template <int RPW, int NV, int UNR>
+__global__ __launch_bounds__(kBlock) void gemv_mlds(const double* __restrict__ A, int64_t lda,
+                                                    const double* __restrict__ X, int64_t ldx,
+                                                    double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                    int64_t K, int nv) {
+    constexpr int NW = kBlock / 64;
+    constexpr int CH2 = 64 * UNR;                 // dbl2 per vector per chunk
+    constexpr int XP = NV * CH2 / kBlock;         // x dbl2 each thread stages per chunk
+    static_assert(XP >= 1 && NV * CH2 % kBlock == 0, "x chunk must split over the workgroup");
+    __shared__ dbl2 xs[2][NV][CH2];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t row0 = (int64_t)blockIdx.x * (NW * RPW) + w * RPW;
+    const double* arow[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    const double* xv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xv[v] = X + (v < nv ? v : 0) * ldx;
+    // the x pairs this thread stages: flat index j = threadIdx.x + kBlock * q over [NV][CH2]
+    const double* xsrc[XP];
+#pragma unroll
+    for (int q = 0; q < XP; ++q) {
+        const int j = threadIdx.x + kBlock * q;
+        xsrc[q] = xv[j / CH2] + 2 * (j % CH2);
+    }
+    double acc[RPW][NV];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[r][v] = 0.0;
+
+    constexpr int64_t kChunk = 128 * UNR;
+    const int64_t nch = K / kChunk;
+    const int64_t c0 = 2 * lane;
+    auto xload = [&](dbl2 (&xr)[XP], int64_t i) {
+#pragma unroll
+        for (int q = 0; q < XP; ++q) xr[q] = load2<false>(xsrc[q] + i * kChunk);
+    };
+    auto xstore = [&](int b, const dbl2 (&xr)[XP]) {
+#pragma unroll
+        for (int q = 0; q < XP; ++q) {
+            const int j = threadIdx.x + kBlock * q;
+            xs[b][j / CH2][j % CH2] = xr[q];
+        }
+    };
+    auto aload = [&](dbl2 (&aa)[RPW][UNR], int64_t i) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) aa[r][u] = load2<true>(arow[r] + i * kChunk + c0 + 128 * u);
+    };
+    auto compute = [&](int b, const dbl2 (&aa)[RPW][UNR]) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const dbl2 xx = xs[b][v][lane + 64 * u];
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    acc[r][v] = __builtin_fma(aa[r][u].x, xx.x, acc[r][v]);
+                    acc[r][v] = __builtin_fma(aa[r][u].y, xx.y, acc[r][v]);
+                }
+            }
+    };
+    if (nch > 0) {
+        dbl2 aa[RPW][UNR], ab[RPW][UNR];
+        dbl2 xr[XP];
+        xload(xr, 0);
+        aload(aa, 0);
+        xstore(0, xr);
+        __syncthreads();
+        int64_t i = 0;  // always even at the top: chunk i sits in aa / xs[0]
+        for (; i + 1 < nch; i += 2) {
+            xload(xr, i + 1);
+            aload(ab, i + 1);
+            compute(0, aa);
+            xstore(1, xr);
+            __syncthreads();
+            if (i + 2 < nch) {
+                xload(xr, i + 2);
+                aload(aa, i + 2);
+                compute(1, ab);
+                xstore(0, xr);
+                __syncthreads();
+            } else {
+                compute(1, ab);
+                i = nch;  // both consumed
+                break;
+            }
+        }
+        if (i < nch) compute(0, aa);
+    }
+    for (int64_t c = nch * kChunk + c0; c < K; c += 128) mtail<RPW, NV>(acc, arow, xv, c, K);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const double s = group_sum<64>(acc[r][v]);
+            if (lane == 0 && row0 + r < M && v < nv) Y[v * ldy + row0 + r] = s;
+        }
+}
+
 typedef void (*gemv_multi_fn)(const double*, int64_t, const double*, int64_t, double*, int64_t, int64_t,
                               int64_t, int);
 
@@ -825,6 +940,11 @@ struct MultiVariant {
 #define MROW(NW, RPB, UNR)                                                                               \
     {"mrow_w" #NW "_r" #RPB "_u" #UNR,                                                                   \
      {gemv_mrow<NW, RPB, 2, UNR>, gemv_mrow<NW, RPB, 4, UNR>, gemv_mrow<NW, RPB, 8, UNR>}, RPB, NW * 64}
+
+#define MLDS(RPW, UNR)                                                                                   \
+    {"mlds_r" #RPW "_u" #UNR,                                                                            \
+     {gemv_mlds<RPW, 2, (UNR > 1 ? UNR : 2)>, gemv_mlds<RPW, 4, UNR>, gemv_mlds<RPW, 8, UNR>},           \
+     (kBlock / 64) * RPW, kBlock}
 
 static const MultiVariant kMultiVariants[] = {
     {"auto", {nullptr, nullptr, nullptr}, 0, 0},  // 0
@@ -849,17 +969,25 @@ static const MultiVariant kMultiVariants[] = {
     MVEC(32, 3, 1),                               // 19
     MROW(4, 8, 1),                                // 20
     MROW(2, 4, 1),                                // 21
+    MLDS(2, 2),                                   // 22
+    MLDS(2, 4),                                   // 23
+    MLDS(4, 2),                                   // 24
+    MLDS(4, 4),                                   // 25
+    MLDS(8, 2),                                   // 26
+    MLDS(1, 4),                                   // 27
+    MLDS(8, 1),                                   // 28
 };
 constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVariants[0]));
 
-// From the MI355X sweeps (tools/multi_bench.py -> profiles/r01/multi_sweep.jsonl; 8 shapes, K = 512
-// ... 65536): per (nv group, K class) the variant with the best geometric mean, within 1.01-1.07x
-// of the best variant per shape (worst 1.17x).
+// From the MI355X sweeps (tools/multi_bench.py -> profiles/r01/multi_sweep.jsonl, then
+// multi_sweep2_lds.jsonl with the LDS form; 8 shapes, K = 512 ... 65536): per (nv group, K class)
+// the variant with the best geometric mean of (rate / best rate on the shape): 0.96-0.99 per
+// class, worst single shape 0.92.
 int pick_multi_variant(int64_t m, int64_t k, int nvp) {
     (void)m;
-    if (nvp <= 2) return k <= 1024 ? 5 : 11;   // mvec_l32_r2_u1 | mrow_w4_r4_u1
-    if (nvp <= 4) return k <= 1024 ? 18 : 21;  // mvec_l16_r3_u1 | mrow_w2_r4_u1
-    return k <= 1024 ? 15 : 16;                // mvec_l16_r4_u1 | mvec_l32_r4_u1
+    if (nvp <= 2) return k <= 1024 ? 5 : 11;                // mvec_l32_r2_u1 | mrow_w4_r4_u1
+    if (nvp <= 4) return k <= 1024 ? 18 : k < 6144 ? 22 : 26;  // mvec_l16_r3_u1 | mlds_r2_u2 | mlds_r8_u2
+    return k <= 1024 ? 15 : k < 6144 ? 22 : 16;             // mvec_l16_r4_u1 | mlds_r2_u2 | mvec_l32_r4_u1
 }
 
 // ------------------------------------------------------------------ other kernels
