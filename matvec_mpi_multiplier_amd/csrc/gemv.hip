@@ -981,8 +981,8 @@ constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVa
 
 // From the MI355X sweeps (tools/multi_bench.py -> profiles/r01/multi_sweep.jsonl, then
 // multi_sweep2_lds.jsonl with the LDS form; 8 shapes, K = 512 ... 65536): per (nv group, K class)
-// the variant with the best geometric mean of (rate / best rate on the shape): 0.96-0.99 per
-// class, worst single shape 0.92.
+// the variant with the best geometric mean of (rate / best rate on the shape): 0.93-0.99 per
+// class, worst single shape 0.90.
 int pick_multi_variant(int64_t m, int64_t k, int nvp) {
     (void)m;
     if (nvp <= 2) return k <= 1024 ? 5 : 11;                // mvec_l32_r2_u1 | mrow_w4_r4_u1
