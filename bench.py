@@ -61,6 +61,7 @@ def parse():
                     help="rows of the sample the real reference runs on (its loop is 100 iterations)")
     ap.add_argument("--ref-timeout", type=float, default=240.0)
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs 3-5 section")
+    ap.add_argument("--configs", default="3,4,5", help="which BASELINE configs the section runs, in order")
     ap.add_argument("--config-steps", type=int, default=20)
     return ap.parse_args()
 
@@ -251,7 +252,8 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
     import torch.distributed as dist
 
     out = []
-    for name, alg, R, C in BASELINE_CONFIGS:
+    by_num = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}
+    for name, alg, R, C in (by_num[int(k)] for k in args.configs.split(",") if k.strip()):
         sh = mm.plan_shard(alg, R, C, n, rank)
         part = R if alg == "colwise" else sh.y_len
         need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + 9 * part + R) + (1 << 30)
