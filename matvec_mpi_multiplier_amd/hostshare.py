@@ -4,6 +4,12 @@ The reference's drivers keep A on the root and scatter it (MPI_Scatter / Pack + 
 host MPICH moves it through shared memory). The MI355X-node form: rank 0 places A in a POSIX
 shared-memory segment, every rank maps it, and each GPU pulls its own shard over its own PCIe
 link (Multiplier.distribute_shared). Collective over the default torch.distributed group.
+
+Page placement is NUMA-aware: the segment is created empty and every rank first-touches (fills)
+its own share of the rows with its threads bound to the CPUs of its GPU's NUMA node, so on a
+two-socket MI355X node each GPU's row shard lands in the DRAM of the socket its PCIe link hangs
+off — the placement an MPI-3 shared window with per-rank segments gives, instead of the whole
+matrix on one socket feeding eight GPUs across the inter-socket link.
 """
 from __future__ import annotations
 
@@ -15,6 +21,34 @@ import numpy as np
 from ._lib import check, lib
 
 SHM_DIR = "/dev/shm"
+
+
+def _cpulist(text: str) -> set[int]:
+    out: set[int] = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.update(range(int(a), int(b) + 1))
+        elif part:
+            out.add(int(part))
+    return out
+
+
+def device_numa_cpus(device: int) -> set[int] | None:
+    """The CPUs (within this process's allowed set) of the NUMA node GPU `device` is attached
+    to, from its PCI address in sysfs; None when unknown (no NUMA info, one node, no overlap)."""
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(device)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        if node < 0:
+            return None
+        cpus = _cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read()) & os.sched_getaffinity(0)
+        return cpus or None
+    except Exception:
+        return None
 
 
 def shm_free_bytes() -> int:
@@ -57,14 +91,27 @@ class SharedHostMatrix:
                 stale.unlink()
                 shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
             me = cls(shm, (R, C), owner=True)
-            if R * C:
-                check(lib.mvg_synth_fill_host(me.array.ctypes.data, C, R, C, 0, 0, C, seed), "mvg_synth_fill_host")
         dist.barrier()
         if dist.get_rank() != 0:
             shm = shared_memory.SharedMemory(name=name)
             # only the creator owns (and unlinks) the segment; Python 3.10 registers attachers too
             resource_tracker.unregister(shm._name, "shared_memory")
             me = cls(shm, (R, C), owner=False)
+        # first touch: rank r fills rows [r*R/n, (r+1)*R/n) from its GPU's NUMA node
+        n, r = dist.get_world_size(), dist.get_rank()
+        r0, r1 = R * r // n, R * (r + 1) // n
+        if r1 > r0 and C:
+            cpus = device_numa_cpus(int(str(device).split(":")[1])) if str(device).startswith("cuda:") else None
+            keep = os.sched_getaffinity(0)
+            if cpus:
+                os.sched_setaffinity(0, cpus)
+            try:
+                check(lib.mvg_synth_fill_host(me.array[r0:].ctypes.data, C, r1 - r0, C, r0, 0, C, seed),
+                      "mvg_synth_fill_host")
+            finally:
+                if cpus:
+                    os.sched_setaffinity(0, keep)
+        dist.barrier()
         return me
 
     def close(self) -> None:
