@@ -186,6 +186,13 @@ int main(int argc, char** argv) {
     if (shared) {
         A = shared;
         x = shared + nA;
+        // NUMA placement before the root fills the window: every rank first-touches its share of
+        // A's rows from its GPU's socket, so each GPU later pulls its shard from local DRAM
+        // instead of one socket's DRAM feeding every GPU across the inter-socket link
+        const int64_t r0 = n_rows * L.rank / L.size, r1 = n_rows * (L.rank + 1) / L.size;
+        (void)mvg_host_first_touch(A + r0 * n_cols, (size_t)(r1 - r0) * (size_t)n_cols * sizeof(double),
+                                   my_device);
+        launch_barrier();
     } else if (root || !ranks) {
         A_own.resize(std::max<size_t>(nA, 1));
         x_own.resize(std::max(n_cols, 1L));

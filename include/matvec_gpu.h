@@ -132,6 +132,12 @@ int mvg_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int mvg_stream_sync(void* stream);
 int mvg_host_register(void* ptr, size_t bytes);     /* pin caller-owned host memory */
 int mvg_host_unregister(void* ptr);
+/* NUMA node of GPU `device` (from its PCI address; -1 when unknown). */
+int mvg_device_numa_node(int device, int* node);
+/* Zero [ptr, ptr + bytes) from threads bound to the CPUs of GPU `device`'s NUMA node, so the
+ * pages land in that socket's DRAM (first-touch placement of host memory the GPU will pull
+ * from; the executables' shared window). Falls back to the caller's CPUs. */
+int mvg_host_first_touch(void* ptr, size_t bytes, int device);
 
 /* ------------------------------------------------------------------ the hot kernel
  * y[i] = sum_j A[i*lda + j] * x[j], i < m, j < k (fp64, row-major, lda >= k).

@@ -97,6 +97,8 @@ SIGNATURES = {
     "mvg_stream_sync": (C.c_int, [_p]),
     "mvg_host_register": (C.c_int, [_p, C.c_size_t]),
     "mvg_host_unregister": (C.c_int, [_p]),
+    "mvg_device_numa_node": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
+    "mvg_host_first_touch": (C.c_int, [_p, C.c_size_t, C.c_int]),
     "mvg_gemv": (C.c_int, [_p, _i64, _p, _p, _i64, _i64, _p]),
     "mvg_gemv_variant": (C.c_int, [_p, _i64, _p, _p, _i64, _i64, C.c_int, _p]),
     "mvg_gemv_variant_count": (C.c_int, []),

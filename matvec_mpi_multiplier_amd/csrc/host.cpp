@@ -1,7 +1,13 @@
 // Host-side parts of the C-ABI: status/error text, device helpers, the synthetic generator
 // on the host, and the shard planner (pure integer work, no GPU needed).
+#include <ctype.h>
 #include <math.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include <string>
 
@@ -276,6 +282,65 @@ int mvg_host_register(void* ptr, size_t bytes) {
     MVG_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
     return MVG_OK;
 }
+// NUMA placement of host memory a GPU will pull from (the shared window of the executables):
+// the pages of [p, p + bytes) are first-touched (zeroed) by threads bound to the CPUs of the
+// NUMA node `device` hangs off (PCI bus id -> sysfs numa_node), so the kernel places them in
+// that socket's DRAM. Placement only: when the node is unknown the caller's CPUs touch them.
+int mvg_device_numa_node(int device, int* node) {
+    if (!node) return fail(MVG_E_INVALID, "null");
+    *node = -1;
+    char bus[64] = {0};
+    MVG_HIP(hipDeviceGetPCIBusId(bus, (int)sizeof bus, device));
+    for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+    char path[160];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (FILE* f = fopen(path, "r")) {
+        if (fscanf(f, "%d", node) != 1) *node = -1;
+        fclose(f);
+    }
+    return MVG_OK;
+}
+
+int mvg_host_first_touch(void* p, size_t bytes, int device) {
+    if (!p || bytes == 0) return MVG_OK;
+    int node = -1;
+    (void)mvg_device_numa_node(device, &node);
+    cpu_set_t keep, want;
+    CPU_ZERO(&want);
+    bool bound = false;
+    if (node >= 0 && pthread_getaffinity_np(pthread_self(), sizeof keep, &keep) == 0) {
+        char path[96];
+        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+        if (FILE* f = fopen(path, "r")) {
+            int a = 0, b = 0;
+            char sep = 0;
+            while (fscanf(f, "%d", &a) == 1) {
+                b = a;
+                if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+                    if (fscanf(f, "%d", &b) != 1) b = a;
+                    if (fscanf(f, "%c", &sep) != 1) sep = 0;
+                }
+                for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+                    if (CPU_ISSET(c, &keep)) CPU_SET(c, &want);
+                if (sep != ',') break;
+            }
+            fclose(f);
+        }
+        // threads created below inherit the calling thread's mask
+        bound = CPU_COUNT(&want) > 0 && pthread_setaffinity_np(pthread_self(), sizeof want, &want) == 0;
+    }
+    const size_t page = 1 << 21;
+    const int64_t chunks = (int64_t)((bytes + page - 1) / page);
+    char* base = (char*)p;
+    parallel_for(chunks, [&](int64_t c0, int64_t c1) {
+        const size_t b0 = (size_t)c0 * page;
+        const size_t b1 = std::min(bytes, (size_t)c1 * page);
+        memset(base + b0, 0, b1 - b0);
+    }, bytes < (64u << 20));
+    if (bound) (void)pthread_setaffinity_np(pthread_self(), sizeof keep, &keep);
+    return MVG_OK;
+}
+
 int mvg_host_unregister(void* ptr) {
     MVG_HIP(hipHostUnregister(ptr));
     return MVG_OK;

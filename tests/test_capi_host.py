@@ -295,3 +295,16 @@ def test_speedup_efficiency_tables(tmp_path):
         assert rows[0] == {"p": 1, "time": 0.002, "speedup": 1.0, "efficiency": 1.0}
         assert rows[1]["speedup"] == pytest.approx(2.0) and rows[1]["efficiency"] == pytest.approx(1.0)
     assert "| 600 | 600 | 4 | 0.000800 | 2.500 | 0.625 |" in stats.table(str(tmp_path / "a.csv"))
+
+
+def test_host_first_touch_zeroes_the_range_without_numa_info():
+    """mvg_host_first_touch (NUMA placement of the executables' shared window) zeroes exactly
+    the given range, in parallel above 64 MiB, and still does so when the GPU's NUMA node cannot
+    be found (no GPU here: the caller's CPUs touch the pages)."""
+    a = np.full(20_000_000, 7.0)  # 160 MB: the threaded path
+    off, n = 1000, 19_000_000
+    assert _lib.lib.mvg_host_first_touch(a[off:].ctypes.data, n * 8, 0) == 0
+    assert not a[off:off + n].any()
+    assert (a[:off] == 7.0).all() and (a[off + n:] == 7.0).all()
+    small = np.full(1000, 3.0)
+    assert _lib.lib.mvg_host_first_touch(small.ctypes.data, small.nbytes, 0) == 0 and not small.any()

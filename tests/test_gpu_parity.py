@@ -381,3 +381,15 @@ def test_distribute_shared_from_dev_shm(comm1, golden, tmp_path):
         assert max_rel(y, golden["sq_480/colwise/P1"]) <= TOL
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_device_numa_node_and_first_touch():
+    """The GPU's NUMA node comes from its PCI address (sysfs); first touch near it zeroes."""
+    import ctypes as C
+
+    node = C.c_int(-2)
+    assert _lib.lib.mvg_device_numa_node(0, C.byref(node)) == 0
+    assert node.value >= -1
+    a = np.full(10_000_000, 1.0)
+    assert _lib.lib.mvg_host_first_touch(a.ctypes.data, a.nbytes, 0) == 0 and not a.any()
