@@ -233,6 +233,8 @@ def _sampled_rows_check(e: "mm.Multiplier", R, Cn, y, rows):
     ("rowwise", 524288, 512),      # config 5's per-GPU shard (4,194,304 x 512 over 8 GPUs)
     ("colwise", 65536, 65536),     # config 3 at G = 1 (32 GiB on the device)
     ("blockwise", 65536, 32768),   # config 4's per-GPU block (131072^2 on a 2 x 4 grid)
+    ("rowwise", 4194304, 512),     # config 5 whole on one GPU (16 GiB)
+    ("blockwise", 131072, 131072),  # config 4 whole on one GPU (1 x 1 grid, 128 GiB)
 ])
 def test_full_size_sampled_rows_and_properties(comm1, alg, R, Cn):
     rng = np.random.default_rng(7)
