@@ -34,6 +34,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -180,7 +181,8 @@ int main(int argc, char** argv) {
     const char* dist_env = getenv("MVG_DIST");
     const bool want_shared = ranks && !(dist_env && strcmp(dist_env, "send") == 0);
     double* shared = want_shared ? (double*)launch_shared_alloc((nA + (size_t)n_cols + 1) * sizeof(double)) : nullptr;
-    std::vector<double> A_own, x_own, y(root ? std::max(n_rows, 1L) : 1);
+    std::vector<double> x_own, y(root ? std::max(n_rows, 1L) : 1);
+    std::unique_ptr<double, decltype(&free)> A_own(nullptr, &free);
     double* A = nullptr;
     double* x = nullptr;
     if (shared) {
@@ -194,10 +196,22 @@ int main(int argc, char** argv) {
                                    my_device);
         launch_barrier();
     } else if (root || !ranks) {
-        A_own.resize(std::max<size_t>(nA, 1));
+        // left untouched by the allocation: the first write decides each page's NUMA node
+        A_own.reset((double*)malloc(std::max<size_t>(nA, 1) * sizeof(double)));
+        if (!A_own) {
+            fprintf(stderr, "out of host memory for A (%zu doubles)\n", nA);
+            return finish(1);
+        }
         x_own.resize(std::max(n_cols, 1L));
-        A = A_own.data();
+        A = A_own.get();
         x = x_own.data();
+        // one process driving G GPUs: GPU g's rows first-touched from GPU g's socket, as the
+        // shared window is in rank mode (one socket's DRAM would otherwise feed every GPU)
+        if (!ranks && comm_sz > 1)
+            for (int g = 0; g < comm_sz; ++g) {
+                const int64_t r0 = n_rows * g / comm_sz, r1 = n_rows * (g + 1) / comm_sz;
+                (void)mvg_host_first_touch(A + r0 * n_cols, (size_t)(r1 - r0) * (size_t)n_cols * sizeof(double), g);
+            }
     }
     if (root) {
         char name[128];
