@@ -923,6 +923,119 @@ __global__ __launch_bounds__(kBlock) void gemv_mlds(const double* __restrict__ A
         }
 }
 
+// x-resident form (short rows, several vectors): the workgroup stages x for all NV vectors in
+// LDS once per 1024-column tile — for K <= 1024 that is all of x, once, behind one barrier —
+// and its lane groups (LPR lanes, RPG rows each, as in gemv_mvec) walk their rows reading x
+// back with ds_read_b128, so the registers hold A (UNR steps double-buffered) and accumulators
+// only, and the vector-memory pipe carries A alone.
+template <int LPR, int RPG, int NV, int UNR>
+__global__ __launch_bounds__(kBlock) void gemv_mxres(const double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ X, int64_t ldx,
+                                                     double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                     int64_t K, int nv) {
+    constexpr int TK = 1024;  // columns per x tile
+    constexpr int G = 64 / LPR;
+    __shared__ dbl2 xs[NV][TK / 2];
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR;
+    const int gl = lane % LPR;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t row0 = (wave * G + g) * RPG;
+    const double* arow[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {
+        int64_t rr = row0 + r;
+        rr = rr < M ? rr : M - 1;
+        arow[r] = A + rr * lda;
+    }
+    double acc[RPG][NV];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[r][v] = 0.0;
+    constexpr int64_t kStep = 2 * LPR;  // columns per step of a lane group
+    constexpr int64_t kChunk = kStep * UNR;
+    auto compute = [&](const dbl2 (&aa)[RPG][UNR], int pbase) {  // pbase: this lane's pair index in the tile
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const dbl2 xx = xs[v][pbase + LPR * u];
+#pragma unroll
+                for (int r = 0; r < RPG; ++r) {
+                    acc[r][v] = __builtin_fma(aa[r][u].x, xx.x, acc[r][v]);
+                    acc[r][v] = __builtin_fma(aa[r][u].y, xx.y, acc[r][v]);
+                }
+            }
+    };
+    auto aload = [&](dbl2 (&aa)[RPG][UNR], int64_t c) {
+#pragma unroll
+        for (int r = 0; r < RPG; ++r)
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) aa[r][u] = load2<true>(arow[r] + c + kStep * u);
+    };
+    for (int64_t t0 = 0; t0 < K; t0 += TK) {
+        const int64_t t1 = K - t0 < TK ? K : t0 + TK;
+        if (t0 > 0) __syncthreads();  // every wave is done with the previous tile
+        for (int j = threadIdx.x; j < NV * (TK / 2); j += kBlock) {
+            const int v = j / (TK / 2), pp = j % (TK / 2);
+            const int64_t c = t0 + 2 * pp;
+            const double* xv = X + (v < nv ? v : 0) * ldx;
+            dbl2 val = {0.0, 0.0};
+            if (c + 1 < t1) val = load2<false>(xv + c);
+            else if (c < t1) val.x = xv[c];
+            xs[v][pp] = val;
+        }
+        __syncthreads();
+        const int64_t nch = (t1 - t0) / kChunk;  // whole chunks in the tile
+        if (nch > 0) {
+            dbl2 aa[RPG][UNR], ab[RPG][UNR];
+            aload(aa, t0 + 2 * gl);
+            int64_t i = 0;
+            for (; i + 1 < nch; i += 2) {
+                aload(ab, t0 + (i + 1) * kChunk + 2 * gl);
+                compute(aa, (int)(i * kChunk / 2) + gl);
+                if (i + 2 < nch) {
+                    aload(aa, t0 + (i + 2) * kChunk + 2 * gl);
+                    compute(ab, (int)((i + 1) * kChunk / 2) + gl);
+                } else {
+                    compute(ab, (int)((i + 1) * kChunk / 2) + gl);
+                    i = nch;
+                    break;
+                }
+            }
+            if (i < nch) compute(aa, (int)(i * kChunk / 2) + gl);
+        }
+        // tile tail: pairs past the whole chunks, then an odd last column (x zero-padded in LDS)
+        for (int64_t c = t0 + nch * kChunk + 2 * gl; c < t1; c += kStep) {
+            const int pp = (int)((c - t0) / 2);
+#pragma unroll
+            for (int r = 0; r < RPG; ++r) {
+                dbl2 a;
+                if (c + 1 < t1) {
+                    a = load2<true>(arow[r] + c);
+                } else {
+                    a.x = arow[r][c];
+                    a.y = 0.0;
+                }
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    const dbl2 xx = xs[v][pp];
+                    acc[r][v] = __builtin_fma(a.x, xx.x, acc[r][v]);
+                    acc[r][v] = __builtin_fma(a.y, xx.y, acc[r][v]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPG; ++r)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const double sum = group_sum<LPR>(acc[r][v]);
+            if (gl == 0 && row0 + r < M && v < nv) Y[v * ldy + row0 + r] = sum;
+        }
+}
+
 typedef void (*gemv_multi_fn)(const double*, int64_t, const double*, int64_t, double*, int64_t, int64_t,
                               int64_t, int);
 
@@ -945,6 +1058,11 @@ struct MultiVariant {
     {"mlds_r" #RPW "_u" #UNR,                                                                            \
      {gemv_mlds<RPW, 2, (UNR > 1 ? UNR : 2)>, gemv_mlds<RPW, 4, UNR>, gemv_mlds<RPW, 8, UNR>},           \
      (kBlock / 64) * RPW, kBlock}
+
+#define MXR(LPR, RPG, UNR)                                                                               \
+    {"mxres_l" #LPR "_r" #RPG "_u" #UNR,                                                                 \
+     {gemv_mxres<LPR, RPG, 2, UNR>, gemv_mxres<LPR, RPG, 4, UNR>, gemv_mxres<LPR, RPG, 8, UNR>},         \
+     (kBlock / 64) * (64 / LPR) * RPG, kBlock}
 
 static const MultiVariant kMultiVariants[] = {
     {"auto", {nullptr, nullptr, nullptr}, 0, 0},  // 0
@@ -976,18 +1094,27 @@ static const MultiVariant kMultiVariants[] = {
     MLDS(8, 2),                                   // 26
     MLDS(1, 4),                                   // 27
     MLDS(8, 1),                                   // 28
+    MXR(16, 4, 1),                                // 29 x resident in LDS
+    MXR(16, 4, 2),                                // 30
+    MXR(32, 4, 1),                                // 31
+    MXR(16, 2, 2),                                // 32
+    MXR(64, 2, 2),                                // 33
+    MXR(32, 2, 2),                                // 34
+    MXR(16, 8, 1),                                // 35
 };
 constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVariants[0]));
 
 // From the MI355X sweeps (tools/multi_bench.py -> profiles/r01/multi_sweep.jsonl, then
-// multi_sweep2_lds.jsonl with the LDS form; 8 shapes, K = 512 ... 65536): per (nv group, K class)
-// the variant with the best geometric mean of (rate / best rate on the shape): 0.93-0.99 per
-// class, worst single shape 0.90.
+// multi_sweep2_lds.jsonl with the LDS form and multi_sweep5_xres.jsonl with the x-resident form;
+// 8 shapes, K = 512 ... 65536): per (nv group, K class) the variant with the best geometric mean
+// of (rate / best rate on the shape): 0.93-1.0 per class, worst single shape 0.90.
 int pick_multi_variant(int64_t m, int64_t k, int nvp) {
     (void)m;
-    if (nvp <= 2) return k <= 1024 ? 5 : 11;                // mvec_l32_r2_u1 | mrow_w4_r4_u1
-    if (nvp <= 4) return k <= 1024 ? 18 : k < 6144 ? 22 : 26;  // mvec_l16_r3_u1 | mlds_r2_u2 | mlds_r8_u2
-    return k <= 1024 ? 15 : k < 6144 ? 22 : 16;             // mvec_l16_r4_u1 | mlds_r2_u2 | mvec_l32_r4_u1
+    // K <= 768: mxres_l16_r4_u2 | mxres_l16_r4_u2 | mxres_l16_r4_u1
+    if (k <= 768) return nvp <= 4 ? 30 : 29;
+    if (nvp <= 2) return k <= 1024 ? 5 : 11;                   // mvec_l32_r2_u1 | mrow_w4_r4_u1
+    if (nvp <= 4) return k <= 1024 ? 34 : k < 6144 ? 22 : 26;  // mxres_l32_r2_u2 | mlds_r2_u2 | mlds_r8_u2
+    return k <= 1024 ? 29 : k < 6144 ? 22 : 16;                // mxres_l16_r4_u1 | mlds_r2_u2 | mvec_l32_r4_u1
 }
 
 // ------------------------------------------------------------------ other kernels
