@@ -9,7 +9,8 @@ at several process counts, and stores rank 0's y (dumped by oracle/ref_dump.h) k
 "<case>/<alg>/P<p>". Only the y vectors (and the two tiny fixture files) are committed;
 synthetic matrices are regenerated bit-exactly from (seed, R, C).
 
-Usage: python tests/golden/make_golden.py   (needs /root/reference and /opt/conda MPICH)
+Usage: python tests/golden/make_golden.py [--only NAME,...]   (needs /root/reference and
+/opt/conda MPICH). --only regenerates just those cases and keeps the others' vectors.
 """
 from __future__ import annotations
 
@@ -41,6 +42,11 @@ CASES = [
     # (multiplier_colwise.c:115 sizes `columns` by n_cols, SURVEY §4 bug 2).
     ("tall_960x96", 960, 96, "synth", {"rowwise": [1, 2, 4, 8], "blockwise": [1, 2, 3, 4, 8]}),
     ("sq_4200", 4200, 4200, "synth", {a: [1, 2, 4, 8] for a in ALL}),
+    # config 2's 16384-row matrix at half its width (1 GiB, 0.95 GB of text): the full 16384^2
+    # makes this MPICH's MPI_Scatter segfault (2^31 bytes in one collective, an int overflow
+    # inside MPICH 3.3.2, not the reference's code)
+    ("big_16384x8192", 16384, 8192, "synth", {"rowwise": [4, 8], "blockwise": [4, 8]}),
+    ("big_8192x16384", 8192, 16384, "synth", {"colwise": [4, 8]}),  # R <= C for the column split
 ]
 
 
@@ -49,21 +55,42 @@ def write_inputs(data_dir: str, name: str, R: int, C: int, source: str) -> None:
         for f in ("matrix_4_8.txt", "vector_8.txt"):
             shutil.copy(os.path.join(HERE, f), os.path.join(data_dir, f))
         return
-    A = oracle.synth(R, C, 42)
     x = oracle.synth(1, C, 4242)[0]
-    np.savetxt(os.path.join(data_dir, f"matrix_{R}_{C}.txt"), A, fmt="%.4f")
+    if R * C > (1 << 24):
+        # large: the library's "%.4f" writer (numpy's savetxt would take minutes); the values
+        # are the same k/10000 the oracle generates, and every test compares against y anyway
+        from matvec_mpi_multiplier_amd import multiplier as mm
+
+        mm.write_matr_synth(os.path.join(data_dir, f"matrix_{R}_{C}.txt"), R, C, 42)
+    else:
+        A = oracle.synth(R, C, 42)
+        np.savetxt(os.path.join(data_dir, f"matrix_{R}_{C}.txt"), A, fmt="%.4f")
     np.savetxt(os.path.join(data_dir, f"vector_{C}.txt"), x, fmt="%.4f")
 
 
 def main() -> None:
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="comma-separated case names to (re)generate")
+    only = [n for n in ap.parse_args().only.split(",") if n]
     subprocess.run([os.path.join(REPO, "oracle", "build_ref.sh")], check=True)
     out: dict[str, np.ndarray] = {}
     manifest = {"generator": "tests/golden/make_golden.py", "reference": "oracle/_ref (MPICH 3.3.2, gcc -O0)",
                 "seed_a": 42, "seed_x": 4242, "cases": []}
+    if only:  # keep every other case's vectors and manifest entry
+        with np.load(os.path.join(HERE, "golden.npz")) as old:
+            out = {k: old[k] for k in old.files if k.split("/")[0] not in only}
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            kept = {c["name"]: c for c in json.load(f)["cases"] if c["name"] not in only}
     with tempfile.TemporaryDirectory() as work:
         data = os.path.join(work, "data")
         os.makedirs(os.path.join(data, "out"))
         for name, R, C, source, plan in CASES:
+            if only and name not in only:
+                if name in kept:
+                    manifest["cases"].append(kept[name])
+                continue
             write_inputs(data, name, R, C, source)
             manifest["cases"].append({"name": name, "R": R, "C": C, "source": source, "runs": plan})
             for alg, plist in plan.items():
@@ -73,7 +100,7 @@ def main() -> None:
                         os.remove(ypath)
                     env = dict(os.environ, ORACLE_Y=ypath)
                     cmd = [MPIEXEC, "-n", str(p), os.path.join(REF_BIN, f"multiplier_{alg}"), str(R), str(C)]
-                    r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=900)
+                    r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=1800)
                     if r.returncode != 0 or not os.path.exists(ypath):
                         raise RuntimeError(f"{name} {alg} P={p} failed: {r.stdout[-500:]} {r.stderr[-500:]}")
                     y = np.loadtxt(ypath, dtype=np.float64, ndmin=1)
