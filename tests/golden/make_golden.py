@@ -43,8 +43,8 @@ CASES = [
     ("tall_960x96", 960, 96, "synth", {"rowwise": [1, 2, 4, 8], "blockwise": [1, 2, 3, 4, 8]}),
     ("sq_4200", 4200, 4200, "synth", {a: [1, 2, 4, 8] for a in ALL}),
     # config 2's 16384-row matrix at half its width (1 GiB, 0.95 GB of text): the full 16384^2
-    # makes this MPICH's MPI_Scatter segfault (2^31 bytes in one collective, an int overflow
-    # inside MPICH 3.3.2, not the reference's code)
+    # segfaults in this build (2^31 bytes through one MPI_Scatter; the reference's own counts
+    # stay below 2^31, so most likely a limit of MPICH 3.3.2)
     ("big_16384x8192", 16384, 8192, "synth", {"rowwise": [4, 8], "blockwise": [4, 8]}),
     ("big_8192x16384", 8192, 16384, "synth", {"colwise": [4, 8]}),  # R <= C for the column split
 ]
