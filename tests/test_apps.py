@@ -213,3 +213,24 @@ def test_bench_two_ranks_one_device(tmp_path):
     assert cfg["config 3"]["shard"] == [65536, 32768] and cfg["config 3"]["value"] > 0
     assert cfg["config 4"]["grid"] == [1, 2] and cfg["config 4"]["shard"] == [131072, 65536]
     assert cfg["config 5"]["shard"] == [2097152, 512] and cfg["config 5"]["value"] > 0
+
+
+# ---- the drop-in contract at 1 GiB: the reference's text format written for a 16384 x 8192
+# matrix (0.95 GB), read by the executables' parallel loader, four ranks under mpiexec (every
+# rank on GPU 0), y against the real reference's own y for the same P.
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,R,C", [("rowwise", 16384, 8192), ("colwise", 8192, 16384), ("blockwise", 16384, 8192)])
+def test_mpiexec_1gib_text_matches_reference(tmp_path, golden, alg, R, C):
+    from matvec_mpi_multiplier_amd import multiplier as mm
+
+    data = tmp_path / "data"
+    (data / "out").mkdir(parents=True)
+    mm.write_matr_synth(str(data / f"matrix_{R}_{C}.txt"), R, C, 42)
+    mm.write_vec(str(data / f"vector_{C}.txt"), mm.synth_host(1, C, 4242)[0])
+    yout = tmp_path / "y.txt"
+    r = mpirun(alg, 4, [R, C], tmp_path, MVG_SAME_DEVICE=1, MVG_ITERS=2, MVG_Y_OUT=yout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Reading matrix from file" in r.stdout
+    name = f"big_{R}x{C}"
+    assert max_rel(np.loadtxt(yout), golden[f"{name}/{alg}/P4"]) <= 1e-12
