@@ -110,7 +110,8 @@ class DeviceBuffer:
 
     def upload(self, a: np.ndarray, stream=None) -> "DeviceBuffer":
         a = np.ascontiguousarray(a, dtype=np.float64)
-        assert a.size <= self.n
+        if a.size > self.n:
+            raise ValueError(f"upload of {a.size} doubles into a buffer of {self.n}")
         check(lib.mvg_memcpy_h2d(self.ptr, a.ctypes.data, a.size * 8, stream), "h2d")
         check(lib.mvg_stream_sync(stream), "sync")
         return self
@@ -162,7 +163,8 @@ def multiply_std_rowwise(A: np.ndarray, x: np.ndarray, variant: int = 0) -> np.n
     A = np.ascontiguousarray(A, dtype=np.float64)
     x = np.ascontiguousarray(x, dtype=np.float64)
     R, Cn = A.shape
-    assert x.shape == (Cn,)
+    if x.shape != (Cn,):
+        raise ValueError(f"x has shape {x.shape}, A has {Cn} columns")
     dA, dx, dy = DeviceBuffer(R * Cn).upload(A), DeviceBuffer(Cn).upload(x), DeviceBuffer(R)
     try:
         gemv(dA.ptr, Cn, dx.ptr, dy.ptr, R, Cn, None, variant)
