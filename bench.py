@@ -41,8 +41,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--alg", default="rowwise", choices=["rowwise", "colwise", "blockwise"])
     ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
     ap.add_argument("--cols", type=int, default=SHARD)
