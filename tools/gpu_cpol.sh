@@ -1,4 +1,6 @@
-# Cache-policy sweep of the buffer-load row-block kernel against the production kernel.
+# Cache-policy sweep of the buffer-load row-block kernel against the production kernel (the record
+# of how profiles/r01/variant_sweep19_cachepolicy.jsonl was made; the rowblkbuf_* experiment
+# variants were dropped afterwards, so today it times only rowblk_w4_r2_u8).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "all_variants" -x -q --timeout 120 --timeout-method thread > gpurun_out/cpol_test.log 2>&1 || { tail -30 gpurun_out/cpol_test.log; exit 1; }
