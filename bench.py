@@ -380,6 +380,7 @@ def cpu_baseline(args, R, C, y_gpu):
     from oracle import ref_runner
 
     P = port["cores"]
+    cpus = port["placement"]["cpus"]
     rows = min(R, args.ref_rows)
     if args.alg in ("rowwise", "blockwise"):
         from oracle import oracle
@@ -390,7 +391,7 @@ def cpu_baseline(args, R, C, y_gpu):
         port["reference"] = "not run: oracle/_ref or mpiexec absent, or the sample does not split"
         return port
     try:
-        r = ref_runner.run(args.alg, rows, C, P, timeout=args.ref_timeout)
+        r = ref_runner.run(args.alg, rows, C, P, timeout=args.ref_timeout, cpus=cpus)
     except Exception as exc:  # the baseline must never sink the bench
         port["reference"] = f"not run: {str(exc)[:300]}"
         return port
@@ -403,7 +404,7 @@ def cpu_baseline(args, R, C, y_gpu):
                       f"(oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its text inputs, its "
                       f"100-iteration loop (distribution from the root + sequential sums + collection); "
                       f"run {r['wall_s']:.1f} s incl. text loading; GPU y matches its y to {rel:.1e}",
-            "host_cpu": host_cpu(),
+            "host_cpu": host_cpu(), "placement": port["placement"]["record"],
             "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")}}
 
 
@@ -427,9 +428,16 @@ def cpu_port_baseline(args, R, C, y_gpu):
         threads -= 1
     A = oracle.synth_block(0, rows, 0, C, C, 42)
     x = oracle.synth(1, C, 4242)[0]
-    t1, y_cpu = oracle.time_multiply(args.alg, A, x, threads, 1)
-    iters = max(2, min(200, int(args.cpu_seconds / max(t1, 1e-6))))
-    t, y_cpu = oracle.time_multiply(args.alg, A, x, threads, iters)
+    # `cores` is enforced, not assumed: the port's threads (and the reference's ranks after it)
+    # run confined to exactly `threads` CPUs, those of the GPU's NUMA node first
+    from oracle import cpuset
+
+    cpus = cpuset.pick(threads, gpu_numa_node())
+    threads = len(cpus)
+    with cpuset.confined(cpus):
+        t1, y_cpu = oracle.time_multiply(args.alg, A, x, threads, 1)
+        iters = max(2, min(200, int(args.cpu_seconds / max(t1, 1e-6))))
+        t, y_cpu = oracle.time_multiply(args.alg, A, x, threads, iters)
     rel = float(np.max(np.abs(y_gpu[:rows] - y_cpu) / np.abs(y_cpu)))
     assert rel <= 1e-12, f"GPU y differs from the reference restatement: {rel}"
     nbytes = 8 * (rows * C + C + rows)
@@ -439,7 +447,21 @@ def cpu_port_baseline(args, R, C, y_gpu):
             "sample": f"{what} ({rows}x{C}) {args.alg}, {threads} threads as ranks, {iters} iterations "
                       f"(reference timing semantics: distribution from the root's A + sequential sums + "
                       f"collection, max over ranks); GPU y matches to {rel:.1e}",
-            "host_cpu": host_cpu()}
+            "host_cpu": host_cpu(), "placement": {"cpus": cpus, "record": cpuset.describe(cpus)}}
+
+
+def gpu_numa_node():
+    from matvec_mpi_multiplier_amd._lib import lib
+    import ctypes
+
+    node = ctypes.c_int(-1)
+    try:
+        dev = int(os.environ.get("LOCAL_RANK", "0"))
+        if lib.mvg_device_numa_node(dev, ctypes.byref(node)) == 0 and node.value >= 0:
+            return node.value
+    except Exception:  # placement is best effort; the CPU count is enforced either way
+        pass
+    return None
 
 
 def _splits(alg, R, C, p):

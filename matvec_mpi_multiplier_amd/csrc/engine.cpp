@@ -477,12 +477,20 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
                 if ((rc = alloc_doubles(&s.stage[0], (int64_t)s.stage_elems)) != MVG_OK) return rc;
                 if ((rc = alloc_doubles(&s.stage[1], (int64_t)s.stage_elems)) != MVG_OK) return rc;
             }
+            // sent[b] starts recorded on s.stream, behind the previous GEMV (which reads dA, dx)
+            // and the exchange wait above: every copy_stream write below is ordered after those
             hipEvent_t copied[2], sent[2];
             for (int b = 0; b < 2; ++b) {
                 MVG_HIP(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
                 MVG_HIP(hipEventCreateWithFlags(&sent[b], hipEventDisableTiming));
                 MVG_HIP(hipEventRecord(sent[b], s.stream));
             }
+            // the own shard's copy into dA/dx needs that order even when no peer piece is sent
+            // (every peer shard empty); waiting on the initial record keeps it overlapping the
+            // last peer sends
+            hipEvent_t ready;
+            MVG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+            MVG_HIP(hipEventRecord(ready, s.stream));
             int buf = 0;
             for (int peer = 1; peer < e->nranks; ++peer) {
                 mvg_shard p;
@@ -513,6 +521,8 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
             }
             // own shard last (MPI_Pack of the root's own strip comes last too, colwise.c:61-69)
             const mvg_shard& p = s.plan;
+            MVG_HIP(hipStreamWaitEvent(s.copy_stream, ready, 0));
+            (void)hipEventDestroy(ready);
             int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.copy_stream);
             if (rc != MVG_OK) return rc;
             if ((rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.copy_stream)) != MVG_OK) return rc;

@@ -454,7 +454,7 @@ struct Variant {
 #define RWQ(NW, RPB, UNR, Q)                                                               \
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xq" #Q, gemv_rowblock<NW, RPB, UNR, true, Q>, RPB, true, NW * 64}
 
-static const Variant kVariants[] = {
+static constexpr Variant kVariants[] = {
     {"auto", nullptr, 0, false},   // 0
     VEC(64, 4, 4, 0, 0),           // 1
     VEC(64, 4, 4, 1, 0),           // 2
@@ -515,6 +515,34 @@ static const Variant kVariants[] = {
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
+// Variants are addressed by name, resolved at compile time: inserting or removing a table
+// entry cannot send a shape to the wrong kernel (a missing name fails the build).
+constexpr bool name_eq(const char* a, const char* b) {
+    while (*a && *a == *b) ++a, ++b;
+    return *a == *b;
+}
+template <typename T, size_t N>
+constexpr int variant_id(const T (&table)[N], const char* name) {
+    for (size_t i = 0; i < N; ++i)
+        if (name_eq(table[i].name, name)) return (int)i;
+    return -1;
+}
+constexpr int kScalarLong = variant_id(kVariants, "scl_l64_r4_u4_nt1");   // 8-B path, K >= 256
+constexpr int kScalarShort = variant_id(kVariants, "scl_l16_r2_u4_nt1");  // 8-B path, K < 256
+constexpr int kSplitK = variant_id(kVariants, "rowblk_w4_r2_u4_splitk");
+constexpr int kRowLong = variant_id(kVariants, "rowblk_w4_r2_u8");
+constexpr int kRowMid = variant_id(kVariants, "rowblk_w8_r2_u4");
+constexpr int kRowSmall = variant_id(kVariants, "rowblk_w2_r2_u4");
+constexpr int kVecTwoRows = variant_id(kVariants, "vec_l64_r2_u4_nt1_o3");
+constexpr int kVecFourRows = variant_id(kVariants, "vec_l64_r4_u4_nt1_o1");
+constexpr int kVecOneRow = variant_id(kVariants, "vec_l64_r1_u4_nt1_o1");
+static_assert(kScalarLong > 0 && !kVariants[kScalarLong].vec, "8-B fallback must not need 16-B loads");
+static_assert(kScalarShort > 0 && !kVariants[kScalarShort].vec, "8-B fallback must not need 16-B loads");
+static_assert(kSplitK > 0 && kVariants[kSplitK].split != nullptr, "split-K variant");
+static_assert(kRowLong > 0 && kRowMid > 0 && kRowSmall > 0 && kVecTwoRows > 0 && kVecFourRows > 0 &&
+                  kVecOneRow > 0,
+              "dispatch names a variant missing from kVariants");
+
 constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4 per CU)
 
 // Shape-adaptive choice, from the round-1 MI355X sweeps (profiles/r01/variant_sweep*.jsonl).
@@ -538,16 +566,16 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 //                     consecutive memory, config 5's shard)
 static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
-    if (!vec) return K >= 256 ? 9 : 10;
+    if (!vec) return K >= 256 ? kScalarLong : kScalarShort;
     const int64_t nrb = (M + 1) / 2;
     if (K >= 8192) {
-        if (nrb < 700) return 48;
-        return K >= 16384 ? 32 : 24;
+        if (nrb < 700) return kSplitK;
+        return K >= 16384 ? kRowLong : kRowMid;
     }
-    if (K > 768 && M * K < (int64_t)(1ll << 27)) return K >= 6144 && nrb >= 700 ? 24 : 33;
-    if (K > 1536) return 15;
-    if (K > 768) return 11;
-    return 19;
+    if (K > 768 && M * K < (int64_t)(1ll << 27)) return K >= 6144 && nrb >= 700 ? kRowMid : kRowSmall;
+    if (K > 1536) return kVecTwoRows;
+    if (K > 768) return kVecFourRows;
+    return kVecOneRow;
 }
 
 // Split-K workspace: one fp64 buffer per (device, stream), grown on demand (growth frees the
@@ -1064,7 +1092,7 @@ struct MultiVariant {
      {gemv_mxres<LPR, RPG, 2, UNR>, gemv_mxres<LPR, RPG, 4, UNR>, gemv_mxres<LPR, RPG, 8, UNR>},         \
      (kBlock / 64) * (64 / LPR) * RPG, kBlock}
 
-static const MultiVariant kMultiVariants[] = {
+static constexpr MultiVariant kMultiVariants[] = {
     {"auto", {nullptr, nullptr, nullptr}, 0, 0},  // 0
     MVEC(16, 1, 1),                               // 1
     MVEC(16, 2, 1),                               // 2
@@ -1108,13 +1136,24 @@ constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVa
 // multi_sweep2_lds.jsonl with the LDS form and multi_sweep5_xres.jsonl with the x-resident form;
 // 8 shapes, K = 512 ... 65536): per (nv group, K class) the variant with the best geometric mean
 // of (rate / best rate on the shape): 0.93-1.0 per class, worst single shape 0.90.
+constexpr int kMx16r4u2 = variant_id(kMultiVariants, "mxres_l16_r4_u2");
+constexpr int kMx16r4u1 = variant_id(kMultiVariants, "mxres_l16_r4_u1");
+constexpr int kMx32r2u2 = variant_id(kMultiVariants, "mxres_l32_r2_u2");
+constexpr int kMv32r2u1 = variant_id(kMultiVariants, "mvec_l32_r2_u1");
+constexpr int kMv32r4u1 = variant_id(kMultiVariants, "mvec_l32_r4_u1");
+constexpr int kMrow4r4u1 = variant_id(kMultiVariants, "mrow_w4_r4_u1");
+constexpr int kMlds2u2 = variant_id(kMultiVariants, "mlds_r2_u2");
+constexpr int kMlds8u2 = variant_id(kMultiVariants, "mlds_r8_u2");
+static_assert(kMx16r4u2 > 0 && kMx16r4u1 > 0 && kMx32r2u2 > 0 && kMv32r2u1 > 0 && kMv32r4u1 > 0 &&
+                  kMrow4r4u1 > 0 && kMlds2u2 > 0 && kMlds8u2 > 0,
+              "multi-vector dispatch names a variant missing from kMultiVariants");
+
 int pick_multi_variant(int64_t m, int64_t k, int nvp) {
     (void)m;
-    // K <= 768: mxres_l16_r4_u2 | mxres_l16_r4_u2 | mxres_l16_r4_u1
-    if (k <= 768) return nvp <= 4 ? 30 : 29;
-    if (nvp <= 2) return k <= 1024 ? 5 : 11;                   // mvec_l32_r2_u1 | mrow_w4_r4_u1
-    if (nvp <= 4) return k <= 1024 ? 34 : k < 6144 ? 22 : 26;  // mxres_l32_r2_u2 | mlds_r2_u2 | mlds_r8_u2
-    return k <= 1024 ? 29 : k < 6144 ? 22 : 16;                // mxres_l16_r4_u1 | mlds_r2_u2 | mvec_l32_r4_u1
+    if (k <= 768) return nvp <= 4 ? kMx16r4u2 : kMx16r4u1;
+    if (nvp <= 2) return k <= 1024 ? kMv32r2u1 : kMrow4r4u1;
+    if (nvp <= 4) return k <= 1024 ? kMx32r2u2 : k < 6144 ? kMlds2u2 : kMlds8u2;
+    return k <= 1024 ? kMx16r4u1 : k < 6144 ? kMlds2u2 : kMv32r4u1;
 }
 
 // ------------------------------------------------------------------ other kernels
@@ -1221,7 +1260,7 @@ int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_
     if (!vec || k == 0) {  // the 8-B path (or k = 0): one vector at a time
         if (variant != 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: variants need even lda/ldx, 16-B aligned A, X");
         for (int v = 0; v < nv; ++v) {
-            int rc = mvg_gemv_variant(A, lda, X + v * ldx, Y + v * ldy, m, k, vec ? 0 : 9, stream);
+            int rc = mvg_gemv_variant(A, lda, X + v * ldx, Y + v * ldy, m, k, vec ? 0 : kScalarLong, stream);
             if (rc != MVG_OK) return rc;
         }
         return MVG_OK;

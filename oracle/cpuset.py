@@ -1,0 +1,78 @@
+"""CPU placement for the CPU baselines — TEST/BENCH INFRASTRUCTURE ONLY.
+
+The CPU baseline reports `cores`; this module makes that number a fact rather than a thread
+count: the reference's MPI ranks (oracle/ref_runner.py) and the port's threads (oracle/oracle.py)
+run with their affinity confined to exactly that many CPUs, and the record carries the CPU list
+and the job's cgroup CPU quota (how many CPUs' worth of time the scheduler grants, whatever
+os.cpu_count() says on a shared host).
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+
+
+def cgroup_cpu_quota() -> dict:
+    """{"cpus": quota / period or None (unlimited), "source": file} from cgroup v2 cpu.max or
+    v1 cpu.cfs_quota_us / cpu.cfs_period_us; {"cpus": None, "source": None} if neither reads."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return {"cpus": None if q == "max" else round(int(q) / int(p), 2), "source": "/sys/fs/cgroup/cpu.max",
+                "raw": f"{q} {p}"}
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return {"cpus": None if q < 0 else round(q / p, 2), "source": "/sys/fs/cgroup/cpu/cpu.cfs_quota_us",
+                "raw": f"{q} {p}"}
+    except (OSError, ValueError):
+        return {"cpus": None, "source": None}
+
+
+def _node_cpus(node: int) -> set[int]:
+    out: set[int] = set()
+    try:
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def pick(n: int, numa_node: int | None = None) -> list[int]:
+    """n CPUs from this process's affinity set: those of `numa_node` first (the GPU's node, so
+    the baseline and the GPU share a socket), then the rest in order. Fewer if fewer exist."""
+    allowed = sorted(os.sched_getaffinity(0))
+    first = [c for c in allowed if numa_node is not None and c in _node_cpus(numa_node)]
+    rest = [c for c in allowed if c not in set(first)]
+    return (first + rest)[:max(1, n)]
+
+
+@contextlib.contextmanager
+def confined(cpus: list[int]):
+    """Confine this process (and the threads it starts meanwhile) to `cpus`; restore after."""
+    before = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, cpus)
+    try:
+        yield
+    finally:
+        os.sched_setaffinity(0, before)
+
+
+def describe(cpus: list[int]) -> dict:
+    return {"cpuset": _ranges(cpus), "cpus_allowed": len(os.sched_getaffinity(0)),
+            "os_cpu_count": os.cpu_count(), "cgroup_quota": cgroup_cpu_quota()}
+
+
+def _ranges(cpus: list[int]) -> str:
+    cpus = sorted(cpus)
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)

@@ -38,10 +38,13 @@ def write_inputs(data_dir: str, R: int, C: int, seed_a: int = 42, seed_x: int = 
           "mvg_write_matr_synth")
 
 
-def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str | None = None) -> dict:
+def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str | None = None,
+        cpus: list[int] | None = None) -> dict:
     """mpiexec -n P multiplier_<alg> R C in a scratch directory. Returns {"seconds": mean time
     per iteration as the reference printed it, "y": rank 0's y, "wall_s": whole run incl. text
-    loading}. Raises RuntimeError on any failure."""
+    loading}. With `cpus`, mpiexec and every rank it starts (MPICH's hydra does not bind by
+    default, so ranks inherit the launcher's affinity) run confined to those CPUs.
+    Raises RuntimeError on any failure."""
     if not available(alg):
         raise RuntimeError(f"reference executable or {MPIEXEC} missing")
     own = workdir is None
@@ -57,7 +60,9 @@ def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str |
         env = dict(os.environ, ORACLE_Y=ypath)
         cmd = [MPIEXEC, "-n", str(P), os.path.join(REF_BIN, f"multiplier_{alg}"), str(R), str(C)]
         t0 = time.perf_counter()
-        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=timeout)
+        pin = (lambda: os.sched_setaffinity(0, cpus)) if cpus else None
+        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=timeout,
+                           preexec_fn=pin)
         wall = time.perf_counter() - t0
         if r.returncode != 0 or not os.path.exists(csv) or not os.path.exists(ypath):
             raise RuntimeError(f"reference {alg} P={P} failed (rc {r.returncode}): {r.stdout[-400:]} {r.stderr[-400:]}")

@@ -15,7 +15,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from oracle import oracle, ref_runner  # noqa: E402
+from oracle import cpuset, oracle, ref_runner  # noqa: E402
 
 
 def host():
@@ -28,7 +28,9 @@ def host():
     except OSError:
         pass
     return {"host_cpu": model, "cpus_visible": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_quota": cpuset.cgroup_cpu_quota(),
+            "binding": "each (alg, P) run confined to P CPUs (sched_setaffinity on mpiexec, inherited by "
+                       "its ranks; the port's P threads likewise); 'cpuset' per line"}
 
 
 def main():
@@ -45,9 +47,10 @@ def main():
     nbytes = 8 * R * C
     for alg in args.algs.split(","):
         for P in (int(p) for p in args.procs.split(",")):
-            line = {"alg": alg, "R": R, "C": C, "P": P}
+            cpus = cpuset.pick(P)
+            line = {"alg": alg, "R": R, "C": C, "P": P, "cpuset": cpuset.describe(cpus)["cpuset"]}
             try:
-                r = ref_runner.run(alg, R, C, P, timeout=900)
+                r = ref_runner.run(alg, R, C, P, timeout=900, cpus=cpus)
                 line.update(ref_ms=round(r["seconds"] * 1e3, 3), ref_GBps=round(nbytes / r["seconds"] / 1e9, 3),
                             ref_wall_s=round(r["wall_s"], 1))
                 y_ref = r["y"]
@@ -55,7 +58,8 @@ def main():
                 line["ref_error"] = str(exc)[:200]
                 y_ref = None
             try:
-                t, y = oracle.time_multiply(alg, A, x, P, 20)
+                with cpuset.confined(cpus):
+                    t, y = oracle.time_multiply(alg, A, x, P, 20)
                 line.update(port_ms=round(t * 1e3, 3), port_GBps=round(nbytes / t / 1e9, 3))
                 if y_ref is not None:
                     line["port_vs_ref_max_rel"] = float(abs(y - y_ref).max() / abs(y_ref).max())
