@@ -365,6 +365,66 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
         eng._keep = None
         del A
         shared.close()
+    # the bound of this path is the GPU's host link, not HBM: report it as a roofline of its own
+    # (per-GPU rate of the slowest rank against the link's spec and a plain pinned H2D copy)
+    link = pcie_roofline(local)
+    if link is not None:
+        best = min((v["mean_s"] for v in (out.get("shared"), out.get("root_send")) if isinstance(v, dict)),
+                   default=None)
+        if best is not None:
+            per_gpu = total_bytes / n_ranks(distributed) / best / 1e9
+            link["achieved"] = round(per_gpu, 2)
+            link["frac"] = round(per_gpu / link["peak"], 4) if link.get("peak") else None
+            link["frac_of_copy"] = round(per_gpu / link["h2d_copy_GBps"], 4)
+        out["roofline"] = link
+    return out
+
+
+def n_ranks(distributed):
+    import torch.distributed as dist
+
+    return dist.get_world_size() if distributed else 1
+
+
+def pcie_roofline(local):
+    """The host link of GPU `local`: its PCIe generation and width from sysfs (peak = the
+    per-direction payload rate after 128b/130b line coding) and the rate of a plain 1 GiB
+    page-locked host -> device copy on it (HIP events), the practical ceiling of distribution."""
+    import torch
+
+    out = {"bound": "pcie", "unit": "GB/s"}
+    try:
+        p = torch.cuda.get_device_properties(local)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        base = f"/sys/bus/pci/devices/{bdf}"
+        speed = open(f"{base}/current_link_speed").read().strip()  # e.g. "32.0 GT/s PCIe"
+        width = int(open(f"{base}/current_link_width").read().strip())
+        gts = float(speed.split()[0])
+        out.update({"link": f"{speed} x{width}", "pci": bdf,
+                    "peak": round(gts * width * (128 / 130) / 8, 2) if gts >= 8 else None})
+    except Exception as exc:  # sysfs layout differs: keep the measured ceiling only
+        out.update({"link": f"unknown ({type(exc).__name__})", "peak": None})
+    try:
+        n = 1 << 27  # 1 GiB of fp64
+        h = torch.empty(n, dtype=torch.float64, pin_memory=True)
+        h.fill_(1.0)
+        d = torch.empty(n, dtype=torch.float64, device=f"cuda:{local}")
+        s = torch.cuda.Stream(device=f"cuda:{local}")
+        best = None
+        with torch.cuda.stream(s):
+            for _ in range(4):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                d.copy_(h, non_blocking=True)
+                e1.record(s)
+                e1.synchronize()
+                ms = e0.elapsed_time(e1)
+                best = ms if best is None else min(best, ms)
+        out["h2d_copy_GBps"] = round(8 * n / (best * 1e-3) / 1e9, 2)
+        del h, d
+    except Exception as exc:
+        log(f"pcie_roofline: copy probe failed: {exc}")
+        return None
     return out
 
 

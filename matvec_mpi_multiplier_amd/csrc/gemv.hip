@@ -51,12 +51,49 @@ __device__ __forceinline__ double group_sum(double v) {
     return v;
 }
 
+// One DPP lane permutation of an fp64 value (two 32-bit v_mov_b32_dpp): a VALU op, no LDS
+// round trip, unlike the ds_bpermute_b32 pair __shfl_xor compiles to.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// Sum over each group of LPR lanes with DPP: quad xor 1, quad xor 2, row half-mirror (8 lanes),
+// row mirror (16 lanes) — after each step every lane of the span holds the same value, since
+// fp64 addition is commutative (a + b == b + a bit for bit) — then one xor-16 shuffle for
+// 32-lane groups, or the four 16-lane row sums read as scalars for the whole wave.
+// Fixed order throughout: deterministic, and the same value in every lane of a group (lane 0
+// of the group stores it; for LPR = 64 the result is wave-uniform).
+template <int LPR>
+__device__ __forceinline__ double group_sum_dpp(double v) {
+    static_assert(LPR == 8 || LPR == 16 || LPR == 32 || LPR == 64, "DPP group size");
+    v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v);  // row_half_mirror
+    if constexpr (LPR >= 16) v += dpp_d<0x140>(v);  // row_mirror
+    if constexpr (LPR == 32) v += __shfl_xor(v, 16, 64);
+    if constexpr (LPR == 64)
+        v = (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+    return v;
+}
+
 constexpr int kBlock = 256;  // 4 waves
 
 // Options of the 16-B kernel (template bit mask).
 constexpr int kPipe = 1;     // software pipeline: chunk i+1's loads issue before chunk i's FMAs
 constexpr int kStagger = 2;  // each wave starts at its own column chunk and wraps around, so the
                              // waves in flight read spread-out columns instead of all the same one
+constexpr int kDpp = 4;      // cross-lane sums with DPP (group_sum_dpp) instead of ds_bpermute
 
 template <int RPG, int UNR, bool NT>
 __device__ __forceinline__ void load_chunk(const double* const (&arow)[RPG], const double* x, int64_t base,
@@ -163,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A,
     }
 #pragma unroll
     for (int r = 0; r < RPG; ++r) {
-        const double s = group_sum<LPR>(acc[r]);
+        const double s = (OPT & kDpp) != 0 ? group_sum_dpp<LPR>(acc[r]) : group_sum<LPR>(acc[r]);
         if (gl == 0 && row0 + r < M) y[row0 + r] = s;
     }
 }
@@ -260,7 +297,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restric
     }
 #pragma unroll
     for (int r = 0; r < RPB; ++r) {
-        const double s = group_sum<64>(acc[r]);
+        const double s = group_sum_dpp<64>(acc[r]);
         if (lane == 0) part[w][r] = s;
     }
     __syncthreads();
@@ -345,7 +382,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock_split(const double* __r
     }
 #pragma unroll
     for (int r = 0; r < RPB; ++r) {
-        const double s = group_sum<64>(acc[r]);
+        const double s = group_sum_dpp<64>(acc[r]);
         if (lane == 0) part[w][r] = s;
     }
     __syncthreads();
@@ -512,6 +549,15 @@ static constexpr Variant kVariants[] = {
     RWQ(4, 2, 8, 256),             // 54
     RWQ(8, 2, 4, 64),              // 55
     RWQ(4, 2, 8, 4),               // 56
+    VEC(64, 1, 4, 1, 5),           // 57 DPP cross-lane sums (kDpp)
+    VEC(64, 1, 8, 1, 4),           // 58
+    VEC(64, 2, 4, 1, 7),           // 59
+    VEC(64, 4, 4, 1, 5),           // 60
+    VEC(32, 1, 4, 1, 5),           // 61
+    VEC(32, 2, 4, 1, 4),           // 62
+    VEC(16, 1, 4, 1, 4),           // 63
+    VEC(16, 2, 4, 1, 4),           // 64
+    VEC(8, 2, 4, 1, 4),            // 65
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -533,9 +579,9 @@ constexpr int kSplitK = variant_id(kVariants, "rowblk_w4_r2_u4_splitk");
 constexpr int kRowLong = variant_id(kVariants, "rowblk_w4_r2_u8");
 constexpr int kRowMid = variant_id(kVariants, "rowblk_w8_r2_u4");
 constexpr int kRowSmall = variant_id(kVariants, "rowblk_w2_r2_u4");
-constexpr int kVecTwoRows = variant_id(kVariants, "vec_l64_r2_u4_nt1_o3");
-constexpr int kVecFourRows = variant_id(kVariants, "vec_l64_r4_u4_nt1_o1");
-constexpr int kVecOneRow = variant_id(kVariants, "vec_l64_r1_u4_nt1_o1");
+constexpr int kVecTwoRows = variant_id(kVariants, "vec_l64_r2_u4_nt1_o7");
+constexpr int kVecFourRows = variant_id(kVariants, "vec_l64_r4_u4_nt1_o5");
+constexpr int kVecOneRow = variant_id(kVariants, "vec_l64_r1_u4_nt1_o5");
 static_assert(kScalarLong > 0 && !kVariants[kScalarLong].vec, "8-B fallback must not need 16-B loads");
 static_assert(kScalarShort > 0 && !kVariants[kScalarShort].vec, "8-B fallback must not need 16-B loads");
 static_assert(kSplitK > 0 && kVariants[kSplitK].split != nullptr, "split-K variant");
@@ -564,6 +610,9 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 //   A >= 1 GiB, K <= 1536   wave-owns-4-rows, pipelined
 //   K <= 768          one row per wave (the whole row is one chunk: 524288 short waves stream
 //                     consecutive memory, config 5's shard)
+// The wave-owns-rows picks finish with DPP sums (kDpp, round 2): within +-0.3 % of the
+// ds_bpermute forms on every swept shape (profiles/r02/variant_sweep_dpp.jsonl) — the
+// reduction was never the limit — and they keep the LDS unit out of the epilogue.
 static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) return K >= 256 ? kScalarLong : kScalarShort;

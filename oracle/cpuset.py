@@ -41,13 +41,42 @@ def _node_cpus(node: int) -> set[int]:
     return out
 
 
+def _cpu_key(c: int, what: str) -> str:
+    try:
+        return open(f"/sys/devices/system/cpu/cpu{c}/{what}").read().strip()
+    except OSError:
+        return str(c)
+
+
+def _spread(cpus: list[int]) -> list[int]:
+    """Order `cpus` so that the first k of them sit on k different physical cores spread
+    round-robin over the L3 domains (CCDs): a memory-bound CPU baseline on n CPUs then gets the
+    bandwidth of as many CCDs as it can reach, not of the one or two that n consecutive CPU
+    numbers share. SMT siblings come after every physical core."""
+    seen_core: set[str] = set()
+    primary, siblings = [], []
+    for c in cpus:
+        core = _cpu_key(c, "topology/thread_siblings_list")
+        (siblings if core in seen_core else primary).append(c)
+        seen_core.add(core)
+    domains: dict[str, list[int]] = {}
+    for c in primary:
+        domains.setdefault(_cpu_key(c, "cache/index3/shared_cpu_list"), []).append(c)
+    rr, lists = [], list(domains.values())
+    for i in range(max((len(v) for v in lists), default=0)):
+        rr.extend(v[i] for v in lists if i < len(v))
+    return rr + siblings
+
+
 def pick(n: int, numa_node: int | None = None) -> list[int]:
     """n CPUs from this process's affinity set: those of `numa_node` first (the GPU's node, so
-    the baseline and the GPU share a socket), then the rest in order. Fewer if fewer exist."""
+    the baseline and the GPU share a socket), then the rest; within each group one CPU per
+    physical core, spread over the L3 domains (`_spread`). Fewer if fewer exist."""
     allowed = sorted(os.sched_getaffinity(0))
-    first = [c for c in allowed if numa_node is not None and c in _node_cpus(numa_node)]
-    rest = [c for c in allowed if c not in set(first)]
-    return (first + rest)[:max(1, n)]
+    node = _node_cpus(numa_node) if numa_node is not None else set()
+    first = [c for c in allowed if c in node]
+    rest = [c for c in allowed if c not in node]
+    return (_spread(first) + _spread(rest))[:max(1, n)]
 
 
 @contextlib.contextmanager

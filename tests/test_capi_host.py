@@ -316,11 +316,11 @@ def test_auto_variant_names_match_the_dispatch_table():
              for m, k in ((16384, 16384), (65536, 32768), (65536, 8192), (524288, 4096), (2097152, 1024),
                           (4194304, 512))}
     assert names[16384] == "rowblk_w4_r2_u8" and names[32768] == "rowblk_w4_r2_u8"
-    assert names[8192] == "rowblk_w8_r2_u4" and names[512] == "vec_l64_r1_u4_nt1_o1"
+    assert names[8192] == "rowblk_w8_r2_u4" and names[512] == "vec_l64_r1_u4_nt1_o5"
     pick = lambda m, k: _lib.lib.mvg_gemv_variant_name(_lib.lib.mvg_gemv_auto_variant(k, m, k)).decode()
     assert pick(120, 60000) == "rowblk_w4_r2_u4_splitk" and pick(1024, 131072) == "rowblk_w4_r2_u4_splitk"
     assert pick(4096, 16384) == "rowblk_w4_r2_u8" and pick(1536, 32768) == "rowblk_w4_r2_u8"
     # below 1 GiB with 768 < K < 8192: row-per-workgroup forms (the reference's test.sh squares)
     assert pick(4200, 4200) == "rowblk_w2_r2_u4" and pick(1800, 1800) == "rowblk_w2_r2_u4"
     assert pick(7800, 7800) == "rowblk_w8_r2_u4" and pick(1024, 6144) == "rowblk_w2_r2_u4"
-    assert names[4096] == "vec_l64_r2_u4_nt1_o3" and names[1024] == "vec_l64_r4_u4_nt1_o1"
+    assert names[4096] == "vec_l64_r2_u4_nt1_o7" and names[1024] == "vec_l64_r4_u4_nt1_o5"
