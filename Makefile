@@ -12,10 +12,10 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 LDLIBS   := -L$(ROCM)/lib -lamdhip64 -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
 
-HIP_SRCS := $(CSRC)/gemv.hip
+HIP_SRCS := $(CSRC)/gemv.hip $(CSRC)/gemv_exact.hip
 CXX_SRCS := $(CSRC)/host.cpp $(CSRC)/engine.cpp $(CSRC)/textio.cpp
 HDRS     := $(CSRC)/common.h include/matvec_gpu.h
-OBJS     := $(BUILD)/gemv.o $(BUILD)/host.o $(BUILD)/engine.o $(BUILD)/textio.o
+OBJS     := $(BUILD)/gemv.o $(BUILD)/gemv_exact.o $(BUILD)/host.o $(BUILD)/engine.o $(BUILD)/textio.o
 APPS     := bin/multiplier_rowwise bin/multiplier_colwise bin/multiplier_blockwise
 
 # The executables' launcher (apps/launch.h): over MPI when one is installed (the image's MPICH
@@ -47,6 +47,10 @@ $(BUILD):
 
 $(BUILD)/gemv.o: $(CSRC)/gemv.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the bit-exact kernels must never fuse a*b + c (the reference rounds the product first)
+$(BUILD)/gemv_exact.o: $(CSRC)/gemv_exact.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -ffp-contract=off -c $< -o $@
 
 $(BUILD)/%.o: $(CSRC)/%.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(CXXFLAGS) -x c++ -c $< -o $@

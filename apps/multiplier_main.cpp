@@ -23,6 +23,8 @@
 //   MVG_SYNTH=1        skip the text files and generate the synthetic inputs (spec in
 //                      include/matvec_gpu.h) on the host — the large configs have no files
 //   MVG_Y_OUT=path     write y, "%.17g" per line (the reference never writes y)
+//   MVG_EXACT=1        bit-exact mode (mvg_engine_set_exact): y, and so the MVG_Y_OUT file, is
+//                      identical to the reference's (its sequential sums and combine orders)
 //   MVG_DATA_DIR=dir   input directory (default ./data, matr_utils.c:45,68)
 //   MVG_ITER_LOG=path  write every timed iteration's end-to-end time (s), one per line
 // Besides the CSV it prints the device-resident time (GEMV + collective only, A resident).

@@ -18,7 +18,10 @@ restatement of its MPI loop on the full matrix beside it; the restatement alone 
 reference cannot run), `end_to_end` (distribution from the root's host memory + multiply + y on
 the root, the reference's timing semantics), and `configs`: BASELINE.json configs 3-5 at their
 own fixed sizes on the same N GPUs (strong scaling, device-resident, same engine, same step),
-so one scaling run covers every multi-GPU config; supplementary, never `value`.
+so one scaling run covers every multi-GPU config; supplementary, never `value`. `exact`: the
+same workload with the engine in bit-exact mode (mvg_engine_set_exact: y identical to the
+reference's sequential sums), its step rate and kernel roofline fraction, and (rank 0, N = 1,
+row split) its y compared bit for bit with the oracle port's and the real reference's.
 """
 from __future__ import annotations
 
@@ -63,6 +66,8 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs 3-5 section")
     ap.add_argument("--configs", default="3,4,5", help="which BASELINE configs the section runs, in order")
     ap.add_argument("--config-steps", type=int, default=20)
+    ap.add_argument("--no-exact", action="store_true",
+                    help="skip the bit-exact section (the same workload with mvg_engine_set_exact)")
     return ap.parse_args()
 
 
@@ -167,6 +172,12 @@ def main():
     if rank == 0:
         assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, "y out of range"
 
+    # ---- the same workload in bit-exact mode (the reference's sequential sums, bit for bit)
+    exact = None
+    y_exact = None
+    if not args.no_exact:
+        exact, y_exact = exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, total_bytes, y)
+
     # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
     e2e = None
     if not args.no_e2e and args.e2e_iters > 0:
@@ -182,7 +193,13 @@ def main():
     # ---- CPU baseline: rank 0 at N = 1 only
     cpu = None
     if rank == 0 and n == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, R, C, y)
+        cpu = cpu_baseline(args, R, C, y, y_exact)
+        same_port, same_ref = cpu.pop("exact_vs_port", None), cpu.pop("exact_vs_reference", None)
+        if exact is not None:
+            # rowwise: the exact y against the oracle port's y (full matrix) and against the real
+            # reference's own y (its sample rows), bit for bit
+            exact["bit_identical_to_port"] = same_port
+            exact["bit_identical_to_reference_sample"] = same_ref
 
     if rank == 0:
         traffic, traffic_src = pmc_traffic(args.alg, R, C, n)
@@ -221,6 +238,7 @@ def main():
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
+            "exact": exact,
             "end_to_end": e2e,
             "configs": configs,
         }
@@ -231,6 +249,55 @@ def main():
     comm.destroy()
     if distributed:
         dist.destroy_process_group()
+
+
+def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, total_bytes, y_tree):
+    """The same workload with the engine in bit-exact mode (mvg_engine_set_exact: every row the
+    reference's own sequential chain of rounded products and adds, mvg_gemv_exact): step rate,
+    the exact kernel's HBM fraction, and its y against the tree-summed y (<= 1e-12). Bit
+    identity with the reference is checked against the oracle port's y in cpu_baseline."""
+    import torch
+    import torch.distributed as dist
+
+    eng.set_exact(True)
+    try:
+        for _ in range(max(2, args.warmup // 4)):
+            eng.multiply()
+        eng.sync()
+        steps = max(10, args.steps // 2)
+        eng.kernel_timing(args.event_every)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.multiply()
+        eng.sync()
+        barrier()
+        el = time.perf_counter() - t0
+        kt = eng.kernel_ms()
+        eng.kernel_timing(0)
+        t = torch.tensor([el, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
+        if distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kms = float(t[0]), float(t[1])
+        y = eng.collect()
+    finally:
+        eng.set_exact(False)
+    out = {"semantics": "mvg_engine_set_exact: y bit-identical to the reference's sequential sums",
+           "value": round(total_bytes * steps / el / 1e9, 1), "unit": "GB/s", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 4), "kernel": exact_kernel_name(eng.shard(0)),
+           "kernel_ms": round(kms, 5),
+           "roofline_frac": round(per_gpu / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None}
+    if rank == 0:
+        rel = float(np.max(np.abs(y - y_tree) / np.abs(y_tree)))
+        assert rel <= 1e-12, f"exact y differs from the tree-summed y by {rel}"
+        out["max_rel_vs_tree"] = rel
+    return out, y
+
+
+def exact_kernel_name(sh) -> str:
+    from matvec_mpi_multiplier_amd._lib import lib
+
+    return lib.mvg_gemv_exact_variant_name(lib.mvg_gemv_exact_auto_variant(sh.n_cols, sh.n_rows, sh.n_cols)).decode()
 
 
 # BASELINE.json configs[2..4], each at its own fixed size (strong scaling over N)
@@ -428,13 +495,13 @@ def pcie_roofline(local):
     return out
 
 
-def cpu_baseline(args, R, C, y_gpu):
+def cpu_baseline(args, R, C, y_gpu, y_exact=None):
     """The reference's CPU path timed on this host. Preferred: the real reference (oracle/_ref,
     built from its own sources, run with MPICH's mpiexec on P = the port's thread count) on the
     leading --ref-rows rows of the same matrix, kind "reference"; its 100-iteration loop is fixed
     in its source. Always also: the oracle port (below), reported under "port" (or as the
     baseline itself, kind "port", when the reference cannot run here)."""
-    port = cpu_port_baseline(args, R, C, y_gpu)
+    port = cpu_port_baseline(args, R, C, y_gpu, y_exact)
     if args.no_ref_baseline:
         return port
     from oracle import ref_runner
@@ -465,10 +532,13 @@ def cpu_baseline(args, R, C, y_gpu):
                       f"100-iteration loop (distribution from the root + sequential sums + collection); "
                       f"run {r['wall_s']:.1f} s incl. text loading; GPU y matches its y to {rel:.1e}",
             "host_cpu": host_cpu(), "placement": port["placement"]["record"],
-            "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")}}
+            "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")},
+            "exact_vs_port": port.get("exact_vs_port"),
+            **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}
+               if y_exact is not None and args.alg == "rowwise" else {})}
 
 
-def cpu_port_baseline(args, R, C, y_gpu):
+def cpu_port_baseline(args, R, C, y_gpu, y_exact=None):
     """The oracle restatement of the reference's CPU path (P threads as MPI ranks, distribution
     from the root's A included, mean of per-iteration max) on this host, on the full workload
     or, above --cpu-sample-bytes, on its leading rows (same values, same algorithm)."""
@@ -500,9 +570,17 @@ def cpu_port_baseline(args, R, C, y_gpu):
         t, y_cpu = oracle.time_multiply(args.alg, A, x, threads, iters)
     rel = float(np.max(np.abs(y_gpu[:rows] - y_cpu) / np.abs(y_cpu)))
     assert rel <= 1e-12, f"GPU y differs from the reference restatement: {rel}"
+    exact_same = None
+    if y_exact is not None and args.alg == "rowwise":
+        # row sums do not depend on the rank count, so the port's P-rank y is the reference's y
+        # for the GPU's single shard too; the exact mode must reproduce it bit for bit (the
+        # column and block splits' combine orders depend on P, and the GPU runs P = N here)
+        exact_same = bool(np.array_equal(y_exact[:rows], y_cpu))
+        assert exact_same, "exact-mode y differs from the reference restatement"
     nbytes = 8 * (rows * C + C + rows)
     what = "full workload" if rows == R else f"sample: leading {rows} of {R} rows"
-    return {"value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+    return {"exact_vs_port": exact_same, "value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
             "ms_per_step": round(t * 1e3, 3), "iters": iters,
             "sample": f"{what} ({rows}x{C}) {args.alg}, {threads} threads as ranks, {iters} iterations "
                       f"(reference timing semantics: distribution from the root's A + sequential sums + "

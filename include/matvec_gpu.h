@@ -13,6 +13,7 @@
  *   mvg_gemv                 <- multiply_std_rowwise          src/matr_utils.c:86-96
  *                               (also the strip GEMV that multiply_colwise computes as
  *                                scale-then-row-sum,          src/multiplier_colwise.c:105-122)
+ *   mvg_gemv_exact           <- the same, bit for bit (the reference's sequential sum)
  *   mvg_grid_shape           <- get_2_most_closest_multipliers src/utils.c:26-37
  *   mvg_plan_shard           <- local_n / local_n_rows / local_n_cols arithmetic
  *                               src/multiplier_rowwise.c:93, src/multiplier_colwise.c:349,
@@ -170,6 +171,23 @@ int mvg_gemv_multi_variant(const double* d_A, int64_t lda, const double* d_X, in
 int mvg_gemv_multi_variant_count(void);
 const char* mvg_gemv_multi_variant_name(int variant);
 
+/* Bit-exact form of mvg_gemv: every row is the reference's own chain
+ *   sum = 0; for j < k: sum = round(sum + round(A[i*lda + j] * x[j]))
+ * (src/matr_utils.c:87-93: a rounded multiply then a rounded add, left to right, no FMA), so
+ * y is bit-identical to multiply_std_rowwise on the same inputs (and to the strip sums of
+ * multiply_colwise, src/multiplier_colwise.c:107-122). One lane per row; rows stream through
+ * LDS (csrc/gemv_exact.hip). Any lda >= k and alignment (16-B aligned A, x with an even lda and
+ * 64*lda*8 < 2^32 take the LDS-DMA path, anything else a per-lane 8-B path). */
+int mvg_gemv_exact(const double* d_A, int64_t lda, const double* d_x, double* d_y,
+                   int64_t m, int64_t k, void* stream);
+/* explicit exact variant (0 = auto; names via mvg_gemv_exact_variant_name: seq_t<T>_b<NB>
+ * LDS-DMA tiles of 2T columns with NB buffers, seq_scalar the 8-B path) */
+int mvg_gemv_exact_variant(const double* d_A, int64_t lda, const double* d_x, double* d_y,
+                           int64_t m, int64_t k, int variant, void* stream);
+int mvg_gemv_exact_variant_count(void);
+int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k);
+const char* mvg_gemv_exact_variant_name(int variant);
+
 /* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */
 int mvg_stream_read(const double* d_src, int64_t n, double* d_sink, void* stream);
 
@@ -224,6 +242,15 @@ int mvg_engine_stream(const mvg_engine* e, int local_index, void** stream);
 int mvg_engine_kernel_timing(mvg_engine* e, int every);
 int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches);
 int mvg_engine_destroy(mvg_engine* e);
+/* Bit-exact mode (off by default; MVG_EXACT=1 in the environment turns it on at creation):
+ * local products by mvg_gemv_exact, and the exchange adds the partials in the reference's own
+ * order — the column split's MPI_Reduce as MPICH's binomial tree in rank order
+ * (colwise.c:124), the block split's partials into a zeroed y in rank order
+ * (blockwise.c:150-207) — after an ncclGather of every partial to rank 0. y is then
+ * bit-identical to the reference's (block split with > 2 grid columns: to the reference's
+ * result for rank-order message arrival; its own order varies run to run). */
+int mvg_engine_set_exact(mvg_engine* e, int on);
+int mvg_engine_exact(const mvg_engine* e, int* on);
 
 /* ------------------------------------------------------------------ text I/O (src/matr_utils.c)
  * Same file names under the same directory convention: <dir>/matrix_<R>_<C>.txt,

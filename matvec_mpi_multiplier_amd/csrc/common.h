@@ -24,6 +24,12 @@ int hip_fail(hipError_t e, const char* what);
         if (_e != hipSuccess) return ::mvg::hip_fail(_e, #call);          \
     } while (0)
 
+// ----- exact exchange (gemv_exact.hip): the reference's own combine orders on the root
+// MPI_Reduce(SUM) as MPICH's binomial tree in rank order (colwise.c:124); overwrites parts
+int launch_combine_binomial(double* parts, int P, int64_t n, double* y, hipStream_t s);
+// gather_local_results (blockwise.c:150-207): y = ((0 + p[gi*gc]) + p[gi*gc+1]) + ... per grid row
+int launch_combine_grid_rows(const double* parts, int gr, int gc, int64_t lr, double* y, hipStream_t s);
+
 // ----- synthetic generator (spec in include/matvec_gpu.h) ---------------------------
 constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ULL;
 

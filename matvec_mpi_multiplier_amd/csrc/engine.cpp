@@ -87,6 +87,7 @@ struct Shard {
     double* dy_row = nullptr;   // block-split row leader: reduced slice (lr doubles)
     double* dy = nullptr;       // rank 0: the full y (R doubles)
     double* stage[2] = {nullptr, nullptr};  // root: staging for root->peer sends (rank mode)
+    double* gbuf = nullptr;     // rank 0, exact mode: every rank's partial, gathered in rank order
     size_t stage_elems = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
@@ -101,6 +102,7 @@ struct mvg_engine {
     bool single_process = false;  // all ranks in this process
     bool always_collect = false;  // run the collectives even at nranks == 1 (tests)
     bool distributed = false;
+    bool exact = false;         // bit-exact mode: mvg_gemv_exact + the reference's combine orders
     int timing_every = 0;       // record kernel events on every Nth multiply (0 = off)
     int64_t nx = 0;             // multiplies with an exchange issued so far
     bool x_pending = false;     // an exchange may still run (slot (nx - 1) % ring)
@@ -137,7 +139,7 @@ void free_shard(Shard& s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.copy_stream) (void)hipStreamSynchronize(s.copy_stream);
     if (s.xstream) (void)hipStreamSynchronize(s.xstream);
-    for (double* p : {s.dA, s.dx, s.dy_row, s.dy, s.stage[0], s.stage[1]})
+    for (double* p : {s.dA, s.dx, s.dy_row, s.dy, s.stage[0], s.stage[1], s.gbuf})
         if (p) (void)hipFree(p);
     for (int b = 0; b < kRing; ++b) {
         if (s.dy_parts[b]) (void)hipFree(s.dy_parts[b]);
@@ -186,6 +188,67 @@ int distribute_direct(mvg_engine* e, const double* A, const double* x) {
         int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
         if (rc != MVG_OK) return rc;
         rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
+        if (rc != MVG_OK) return rc;
+    }
+    return MVG_OK;
+}
+
+// The exchange step from the shared schedule (mvg_plan_exchange). A failing call inside the
+// group still closes the group before the error is reported.
+int exchange_plan(mvg_engine* e, int b, bool serial) {
+    const int nsteps = e->shards[0].nsteps;
+    for (int k = 0; k < nsteps; ++k) {
+        MVG_NCCL(ncclGroupStart());
+        ncclResult_t r = ncclSuccess;
+        const char* what = "";
+        for (auto& s : e->shards) {
+            const mvg_xstep& st = s.steps[k];
+            if (!st.member) continue;
+            (void)hipSetDevice(s.device);
+            double* bufs[3] = {s.dy_parts[b], s.dy_row, s.dy};
+            const double* src = bufs[st.src];
+            double* dst = bufs[st.dst];
+            if (!dst) dst = s.dy_parts[b];  // recvbuff is only written on the root
+            if (st.op == MVG_X_GATHER) {
+                r = ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
+                what = "ncclGather";
+            } else {
+                r = ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
+                what = "ncclReduce";
+            }
+            if (r != ncclSuccess) break;
+        }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return nccl_fail(r, what);
+        if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
+    }
+    return MVG_OK;
+}
+
+// Exact mode (mvg_engine_set_exact): every partial gathered to rank 0 in rank order, then added
+// there in the reference's order.
+int exchange_exact(mvg_engine* e, int b, bool serial) {
+    const int64_t count = e->alg == MVG_ALG_COLWISE ? e->R : e->shards[0].plan.y_len;
+    MVG_NCCL(ncclGroupStart());
+    ncclResult_t r = ncclSuccess;
+    for (auto& s : e->shards) {
+        (void)hipSetDevice(s.device);
+        // recvbuff is only written on the root
+        r = ncclGather(s.dy_parts[b], s.rank == 0 ? s.gbuf : s.dy_parts[b], (size_t)count, ncclFloat64, 0,
+                       s.world, serial ? s.stream : s.xstream);
+        if (r != ncclSuccess) break;
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGather (exact)");
+    if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
+    for (auto& s : e->shards) {
+        if (s.rank != 0) continue;
+        MVG_HIP(hipSetDevice(s.device));
+        hipStream_t st = serial ? s.stream : s.xstream;
+        const int rc = e->alg == MVG_ALG_COLWISE
+                           ? launch_combine_binomial(s.gbuf, e->nranks, e->R, s.dy, st)
+                           : launch_combine_grid_rows(s.gbuf, s.plan.grid_rows, s.plan.grid_cols, s.plan.y_len,
+                                                      s.dy, st);
         if (rc != MVG_OK) return rc;
     }
     return MVG_OK;
@@ -301,6 +364,8 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
     // variable has none)
     e->always_collect = ac && ac[0] == '1' && comm->locals[0].comm != nullptr;
     if (const char* v = getenv("MVG_XRING")) e->ring = std::max(1, std::min(kRing, atoi(v)));
+    const char* ex = getenv("MVG_EXACT");
+    const bool want_exact = ex && ex[0] == '1';
 
     e->shards.resize(comm->locals.size());
     auto bail = [&](int code) {
@@ -407,7 +472,38 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit"));
         if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit group"));
     }
+    if (want_exact && (rc = mvg_engine_set_exact(e, 1)) != MVG_OK) return bail(rc);
     *out = e;
+    return MVG_OK;
+}
+
+// Exact mode: the local products come from mvg_gemv_exact (the reference's sequential sums) and
+// the exchange reproduces the reference's combine order instead of RCCL's: every rank's partial
+// is gathered to rank 0 in rank order (one ncclGather) and a small kernel there adds them as
+// the reference does — MPI_Reduce's binomial tree for the column split (colwise.c:124), the
+// grid row's blocks into a zeroed y in rank order for the block split (blockwise.c:150-207).
+// The row split's gather is a copy and stays as it is. y is then bit-identical to the
+// reference's (block split: to its result for rank-order arrival, which is every arrival order
+// when the grid has at most two columns).
+int mvg_engine_set_exact(mvg_engine* e, int on) {
+    if (!e) return fail(MVG_E_INVALID, "null engine");
+    int rc = mvg_engine_sync(e);
+    if (rc != MVG_OK) return rc;
+    e->exact = on != 0;
+    if (!e->exact || e->alg == MVG_ALG_ROWWISE) return MVG_OK;
+    DeviceGuard g;
+    for (auto& s : e->shards) {
+        if (s.rank != 0 || s.nsteps == 0 || s.gbuf) continue;
+        MVG_HIP(hipSetDevice(s.device));
+        const int64_t part = e->alg == MVG_ALG_COLWISE ? e->R : s.plan.y_len;
+        if ((rc = alloc_doubles(&s.gbuf, part * e->nranks)) != MVG_OK) return rc;
+    }
+    return MVG_OK;
+}
+
+int mvg_engine_exact(const mvg_engine* e, int* on) {
+    if (!e || !on) return fail(MVG_E_INVALID, "null");
+    *on = e->exact ? 1 : 0;
     return MVG_OK;
 }
 
@@ -606,7 +702,8 @@ int mvg_engine_multiply(mvg_engine* e) {
             ++s.ev_used;
             MVG_HIP(hipEventRecord(t0, s.stream));
         }
-        int rc = mvg_gemv(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream);
+        int rc = e->exact ? mvg_gemv_exact(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream)
+                          : mvg_gemv(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream);
         if (rc != MVG_OK) return rc;
         if (timed) MVG_HIP(hipEventRecord(t1, s.stream));
         if (!solo && !serial) {
@@ -615,34 +712,9 @@ int mvg_engine_multiply(mvg_engine* e) {
         }
     }
     if (solo) return MVG_OK;
-    // 2) the exchange step, from the shared schedule (mvg_plan_exchange), on the exchange
-    // stream: it overlaps the next multiply's GEMV. A failing call inside the group still closes
-    // the group before the error is reported.
-    for (int k = 0; k < nsteps; ++k) {
-        MVG_NCCL(ncclGroupStart());
-        ncclResult_t r = ncclSuccess;
-        const char* what = "";
-        for (auto& s : e->shards) {
-            const mvg_xstep& st = s.steps[k];
-            if (!st.member) continue;
-            (void)hipSetDevice(s.device);
-            double* bufs[3] = {s.dy_parts[b], s.dy_row, s.dy};
-            const double* src = bufs[st.src];
-            double* dst = bufs[st.dst];
-            if (!dst) dst = s.dy_parts[b];  // recvbuff is only written on the root
-            if (st.op == MVG_X_GATHER) {
-                r = ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
-                what = "ncclGather";
-            } else {
-                r = ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
-                what = "ncclReduce";
-            }
-            if (r != ncclSuccess) break;
-        }
-        const ncclResult_t r2 = ncclGroupEnd();
-        if (r != ncclSuccess) return nccl_fail(r, what);
-        if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
-    }
+    // 2) the exchange step on the exchange stream, overlapping the next multiply's GEMV
+    const int rc_x = e->exact && e->alg != MVG_ALG_ROWWISE ? exchange_exact(e, b, serial) : exchange_plan(e, b, serial);
+    if (rc_x != MVG_OK) return rc_x;
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
         if (!serial) MVG_HIP(hipEventRecord(s.x_done[b], s.xstream));

@@ -1,0 +1,329 @@
+// Bit-exact fp64 GEMV for gfx950: the reference's own arithmetic at HBM speed.
+//
+// multiply_std_rowwise (reference src/matr_utils.c:86-96) computes every row as
+//     sum = 0; for j in 0..K-1: sum = round(sum + round(A[i][j] * x[j]))
+// — a strictly sequential chain, a rounded multiply then a rounded add (no FMA: gcc on x86-64
+// does not contract), and multiply_colwise (src/multiplier_colwise.c:107-122) does the same on a
+// strip (scale in place = the rounded product, then the left-to-right row sum from 0.0). The
+// tree-summed kernels in gemv.hip match that to ~1e-15; the kernels here reproduce it bit for
+// bit, so y (and the `%.17g` y file) is identical to the reference's.
+//
+// A sequential chain cannot be split over lanes, so one lane owns one row for the whole of K.
+// Reading A that way directly (64 lanes -> 64 rows per load instruction) would defeat
+// coalescing; instead each one-wave workgroup owns 64 consecutive rows and streams them through
+// LDS in tiles of 64 rows x 2T columns:
+//   load  : T `global_load_lds_dwordx4` per tile (LDS-DMA, no VGPRs, nt): instruction i fills
+//           rows [i*64/T, +64/T) of the tile, every row segment a contiguous 16*T bytes of A;
+//   read  : lane l takes row l's 16-B chunks in column order with `ds_read_b128`;
+//   swizzle: a lane-linear LDS image would put chunk k of all 64 rows in the same bank group,
+//           so the source address of LDS slot s in row r is chunk s ^ (r & 15) and the read of
+//           chunk k goes to slot k ^ (l & 15) — the same involution on both sides, conflict-free
+//           over every ds_read_b128 lane group (rule 21 of the HIP guide);
+//   x     : the tile's x values are wave-uniform, read through the scalar cache into SGPRs and
+//           used as v_mul_f64 operands;
+//   pipeline: NB tile buffers per wave, NB-1 tiles' loads in flight behind the one being summed,
+//           retired with a counted `s_waitcnt vmcnt(T*(NB-1))` (hipcc does not track LDS-DMA).
+// Rows past M re-read row M-1 (never stored); the column tail K % 2T and any A that is not
+// 16-B aligned with an even lda take per-lane 8-B loads in the same column order.
+#include "common.h"
+
+// hipcc contracts a*b + c into an FMA by default (-ffp-contract=fast); the reference rounds the
+// product first. Off for this whole file (the Makefile also passes -ffp-contract=off for it).
+#pragma clang fp contract(off)
+
+namespace mvg {
+
+typedef double dbl2x __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* gbl_void_t;
+
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8]; the
+// others left at "no wait"), fenced against compiler reordering of memory operations: the
+// LDS-DMA writes of the tile about to be read are complete once at most N vector-memory
+// operations of this wave are outstanding. (The builtin rather than inline asm: a kernel with
+// inline asm is assumed to use every AGPR, which halves occupancy.)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx950");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void wait_lgkmcnt0() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// The reference's step: a rounded product, then a rounded add (never fused: plain operators
+// under the pragma above; HIP's __dmul_rn/__dadd_rn are defined where contraction is on, and
+// the backend fuses them after inlining).
+__device__ __forceinline__ double seq_step(double sum, double a, double x) {
+    const double p = a * x;
+    return sum + p;
+}
+
+template <int RW, int T, int NB>
+__global__ __launch_bounds__(64) void gemv_seq(const double* __restrict__ A, int64_t lda,
+                                               const double* __restrict__ x,
+                                               double* __restrict__ y, int64_t M, int64_t K) {
+    static_assert(RW == 16 || RW == 32 || RW == 64, "rows per wave");
+    static_assert(T >= 16 && T <= 64 && (T & (T - 1)) == 0, "tile width: 16..64 chunks");
+    constexpr int kRows = 64 / T;          // rows one LDS-DMA instruction fills (1 KiB)
+    constexpr int kInst = RW / kRows;      // LDS-DMA instructions per tile
+    static_assert(kInst * kRows == RW, "a tile is whole instructions");
+    static_assert(NB >= 2 && kInst * (NB - 1) <= 63, "loads in flight must fit the vmcnt counter");
+    constexpr int kCols = 2 * T;           // columns per tile
+    constexpr int kRowBytes = 16 * T;      // LDS row stride
+    constexpr int kTileBytes = RW * kRowBytes;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NB * kTileBytes];
+
+    const int lane = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * RW;
+    const int64_t ntiles = K / kCols;
+
+    // load side: instruction i, lane -> tile row i*kRows + lane/T (clamped to the last row),
+    // LDS slot lane%T, which holds the row's chunk slot ^ (row & 15). Addresses are a
+    // wave-uniform base (this tile's columns of row r0, in SGPRs) plus a 32-bit per-lane byte
+    // offset (the caller guarantees 64 rows of lda fit 32 bits).
+    uint32_t off[kInst];
+#pragma unroll
+    for (int i = 0; i < kInst; ++i) {
+        const int row = i * kRows + lane / T;
+        const int64_t rr = r0 + row < M ? row : M - 1 - r0;
+        off[i] = (uint32_t)((rr * lda + 2 * ((lane % T) ^ (row & 15))) * (int64_t)sizeof(double));
+    }
+    const unsigned char* const a0 = reinterpret_cast<const unsigned char*>(A + r0 * lda);
+    auto issue = [&](int64_t t, int b) {
+        const unsigned char* base = a0 + t * kCols * (int64_t)sizeof(double);
+#pragma unroll
+        for (int i = 0; i < kInst; ++i)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(base + off[i]),
+                                             (lds_void_t)(lds + b * kTileBytes + i * 1024), 16, 0,
+                                             2 /* nt */);
+    };
+
+    // compute side: lane l sums tile row l % RW (with RW < 64 the upper lanes repeat rows and
+    // store nothing); row r's chunk k sits at slot k ^ (r & 15): base_r ^ (k << 4)
+    const int myr = lane % RW;
+    double sum = 0.0;
+    const uint32_t my_row = (uint32_t)(myr * kRowBytes + ((myr & 15) << 4));
+    auto consume = [&](int64_t t, int b) {
+        const double* xt = x + t * kCols;
+        const unsigned char* tile = lds + b * kTileBytes;
+        // groups of 16 chunks: the group's LDS reads issue together, then its 32 steps
+#pragma unroll
+        for (int g = 0; g < T; g += 16) {
+            dbl2x a[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                a[k] = *reinterpret_cast<const dbl2x*>(tile + (my_row ^ (uint32_t)((g + k) << 4)));
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                sum = seq_step(sum, a[k].x, xt[2 * (g + k)]);
+                sum = seq_step(sum, a[k].y, xt[2 * (g + k) + 1]);
+            }
+        }
+    };
+
+    for (int p = 0; p < NB - 1; ++p)
+        if (p < ntiles) issue(p, p);
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int64_t tn = t + NB - 1;
+        if (tn < ntiles) {
+            // buffer tn % NB was summed in iteration t-1; its ds_reads have returned (their
+            // values fed the adds), the wait only keeps the order explicit
+            wait_lgkmcnt0();
+            issue(tn, (int)(tn % NB));
+            wait_vmcnt<kInst*(NB - 1)>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        consume(t, (int)(t % NB));
+    }
+    // column tail, same order
+    int64_t rr = r0 + myr;
+    rr = rr < M ? rr : M - 1;
+    const double* arow = A + rr * lda;
+    for (int64_t j = ntiles * kCols; j < K; ++j) sum = seq_step(sum, arow[j], x[j]);
+    if (lane < RW && r0 + lane < M) y[r0 + lane] = sum;
+}
+
+// Any alignment, any lda: lane = row, 8-B loads walking the row (uncoalesced; small or odd
+// shapes only).
+__global__ __launch_bounds__(64) void gemv_seq_scalar(const double* __restrict__ A, int64_t lda,
+                                                      const double* __restrict__ x,
+                                                      double* __restrict__ y, int64_t M, int64_t K) {
+    const int64_t row = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    const int64_t rr = row < M ? row : M - 1;
+    const double* arow = A + rr * lda;
+    double sum = 0.0;
+    int64_t j = 0;
+    for (; j + 4 <= K; j += 4) {
+        const double a0 = arow[j], a1 = arow[j + 1], a2 = arow[j + 2], a3 = arow[j + 3];
+        sum = seq_step(sum, a0, x[j]);
+        sum = seq_step(sum, a1, x[j + 1]);
+        sum = seq_step(sum, a2, x[j + 2]);
+        sum = seq_step(sum, a3, x[j + 3]);
+    }
+    for (; j < K; ++j) sum = seq_step(sum, arow[j], x[j]);
+    if (row < M) y[row] = sum;
+}
+
+// ------------------------------------------------------------------ exact combines
+// MPI_Reduce(SUM) as MPICH 3.3 runs it for a commutative op (the reference's colwise.c:124):
+// a binomial tree in rank order, ((p0 + p1) + (p2 + p3)) + ..., parts[r*n + i] = rank r's
+// partial. Overwrites parts; y[i] = the root's result.
+__global__ void combine_binomial(double* __restrict__ parts, int P, int64_t n, double* __restrict__ y) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        for (int mask = 1; mask < P; mask <<= 1)
+            for (int r = 0; r + mask < P; r += 2 * mask)
+                parts[r * n + i] = parts[r * n + i] + parts[(r + mask) * n + i];
+        y[i] = parts[i];
+    }
+}
+
+// gather_local_results (blockwise.c:150-207): y starts at 0 and every block's partial of the
+// grid row is added in rank order (the root's own first; the reference takes the others in
+// MPI_ANY_SOURCE arrival order, which for two grid columns gives the same sum). parts[r*lr + j]
+// = rank r's partial; y[gi*lr + j] = ((0 + p[gi*gc]) + p[gi*gc + 1]) + ...
+__global__ void combine_grid_rows(const double* __restrict__ parts, int gr, int gc, int64_t lr,
+                                  double* __restrict__ y) {
+    const int64_t n = (int64_t)gr * lr;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t gi = idx / lr, j = idx % lr;
+        double s = 0.0;
+        for (int c = 0; c < gc; ++c) s = s + parts[(gi * gc + c) * lr + j];
+        y[idx] = s;
+    }
+}
+
+int launch_combine_binomial(double* parts, int P, int64_t n, double* y, hipStream_t s) {
+    if (n <= 0) return MVG_OK;
+    const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+    hipLaunchKernelGGL(combine_binomial, dim3((unsigned)blocks), dim3(256), 0, s, parts, P, n, y);
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
+}
+
+int launch_combine_grid_rows(const double* parts, int gr, int gc, int64_t lr, double* y, hipStream_t s) {
+    const int64_t n = (int64_t)gr * lr;
+    if (n <= 0) return MVG_OK;
+    const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+    hipLaunchKernelGGL(combine_grid_rows, dim3((unsigned)blocks), dim3(256), 0, s, parts, gr, gc, lr, y);
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
+}
+
+// ------------------------------------------------------------------ variant table
+typedef void (*seq_fn)(const double*, int64_t, const double*, double*, int64_t, int64_t);
+struct SeqVariant {
+    const char* name;
+    seq_fn fn;
+    bool vec;  // LDS-DMA path: needs 16-B aligned A, x and an even lda
+    int rows;  // rows per one-wave workgroup
+};
+
+#define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, true, RW}
+static constexpr SeqVariant kSeqVariants[] = {
+    {"auto", nullptr, false, 64},          // 0
+    {"seq_scalar", gemv_seq_scalar, false, 64},
+    SEQ(64, 16, 2),   // LDS per wave: NB x RW x 16T bytes; 32 KiB
+    SEQ(64, 16, 3),   // 48 KiB
+    SEQ(64, 16, 4),   // 64 KiB
+    SEQ(64, 32, 2),   // 64 KiB
+    SEQ(32, 32, 2),   // 32 KiB
+    SEQ(32, 32, 3),   // 48 KiB
+    SEQ(32, 64, 2),   // 64 KiB
+    SEQ(16, 64, 2),   // 32 KiB
+    SEQ(16, 64, 3),   // 48 KiB
+    SEQ(16, 64, 4),   // 64 KiB
+    SEQ(16, 32, 4),   // 32 KiB
+};
+constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
+
+// the LDS-DMA path's per-lane offsets span 64 rows of lda in 32 bits
+static bool seq_vec_ok(int64_t lda, bool aligned) { return aligned && lda % 2 == 0 && lda < (1ll << 23); }
+
+template <size_t N>
+constexpr int seq_id(const SeqVariant (&table)[N], const char* name) {
+    for (size_t i = 0; i < N; ++i) {
+        const char *a = table[i].name, *b = name;
+        while (*a && *a == *b) ++a, ++b;
+        if (*a == *b) return (int)i;
+    }
+    return -1;
+}
+constexpr int kSeqScalar = seq_id(kSeqVariants, "seq_scalar");
+constexpr int kSeqR64T16 = seq_id(kSeqVariants, "seq_r64_t16_b2");
+constexpr int kSeqR64T32 = seq_id(kSeqVariants, "seq_r64_t32_b2");
+constexpr int kSeqR32T64 = seq_id(kSeqVariants, "seq_r32_t64_b2");
+constexpr int kSeqR16T64 = seq_id(kSeqVariants, "seq_r16_t64_b2");
+static_assert(kSeqScalar > 0 && !kSeqVariants[kSeqScalar].vec, "8-B exact fallback");
+static_assert(kSeqR64T16 > 0 && kSeqR64T32 > 0 && kSeqR32T64 > 0 && kSeqR16T64 > 0,
+              "exact dispatch names a missing variant");
+
+// From the round-2 MI355X sweep (tools/sweep_exact.py -> profiles/r02/sweep_exact.jsonl). A lane
+// owns a row, so the row count sets the waves: with >= 65536 rows (>= 4 waves of 64 rows per
+// CU) 64-row waves with 256-B row segments per tile (7.0 TB/s at 65536^2 and 65536 x 32768,
+// 0.96-0.97 of the tree-summed kernel), 512-B segments when rows are short (K <= 1024: 4194304 x
+// 512 at 6.9 TB/s, level with the tree kernel on that box); 16384-65535 rows: 32-row waves with
+// 1-KiB segments (16384^2 at 6.5 TB/s); fewer: 16-row waves (the upper 48 lanes repeat rows).
+static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
+    if (!seq_vec_ok(lda, aligned)) return kSeqScalar;
+    if (M >= 65536) return K <= 1024 ? kSeqR64T32 : kSeqR64T16;
+    return M >= 16384 ? kSeqR32T64 : kSeqR16T64;
+}
+
+}  // namespace mvg
+
+using namespace mvg;
+
+extern "C" {
+
+int mvg_gemv_exact_variant_count(void) { return kNumSeqVariants; }
+
+const char* mvg_gemv_exact_variant_name(int v) {
+    if (v < 0 || v >= kNumSeqVariants) return "invalid";
+    return kSeqVariants[v].name;
+}
+
+int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k) { return pick_seq_variant(lda, m, k, true); }
+
+int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
+                           int variant, void* stream) {
+    if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact: negative size");
+    if (variant < 0 || variant >= kNumSeqVariants || (variant > 0 && !kSeqVariants[variant].fn))
+        return fail(MVG_E_INVALID, "mvg_gemv_exact: bad variant");
+    if (m == 0) return MVG_OK;
+    if (!y) return fail(MVG_E_INVALID, "mvg_gemv_exact: null y");
+    hipStream_t s = (hipStream_t)stream;
+    if (k > 0) {
+        if (!A || !x) return fail(MVG_E_INVALID, "mvg_gemv_exact: null A or x");
+        if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv_exact: lda < k");
+    }
+    const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
+    const int v = variant == 0 ? pick_seq_variant(lda, m, k, aligned) : variant;
+    if (kSeqVariants[v].vec && !seq_vec_ok(lda, aligned))
+        return fail(MVG_E_INVALID, "mvg_gemv_exact: LDS-DMA variant needs 16-B aligned A, x and an even lda < 2^23");
+    // k == 0 runs the kernel too: every row's sum stays 0 (the reference's `sum = 0`)
+    // grid-size cap: fewer than 2^32 threads per launch
+    const int64_t max_rows = ((1ll << 26) - 1) * kSeqVariants[v].rows;
+    for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
+        const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
+        const int rw = kSeqVariants[v].rows;
+        hipLaunchKernelGGL(kSeqVariants[v].fn, dim3((unsigned)((mm + rw - 1) / rw)), dim3(64), 0, s,
+                           A ? A + r0 * lda : A, lda, x, y + r0, mm, k);
+        MVG_HIP(hipGetLastError());
+    }
+    return MVG_OK;
+}
+
+int mvg_gemv_exact(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
+                   void* stream) {
+    return mvg_gemv_exact_variant(A, lda, x, y, m, k, 0, stream);
+}
+
+}  // extern "C"

@@ -2,7 +2,8 @@
 
 Reference names are kept so a user of the MPI lab code finds the same operations:
 
-  multiply_std_rowwise(A, x)          src/matr_utils.c:86-96   (runs the HIP GEMV on cuda:0)
+  multiply_std_rowwise(A, x)          src/matr_utils.c:86-96   (runs the HIP GEMV on cuda:0;
+                                      exact=True: bit-identical to the reference's sum)
   get_2_most_closest_multipliers(p)   src/utils.c:26-37
   load_matr / load_vec                src/matr_utils.c:42-83   (same file names, "%lf" tokens)
   build_matrix_filename / build_vector_filename   src/matr_utils.c:9-18
@@ -135,9 +136,13 @@ class DeviceBuffer:
             pass
 
 
-def gemv(d_A: int, lda: int, d_x: int, d_y: int, m: int, k: int, stream=None, variant: int = 0) -> None:
-    """y = A x on device pointers (the raw kernel, mvg_gemv)."""
-    check(lib.mvg_gemv_variant(d_A, lda, d_x, d_y, m, k, variant, stream), "mvg_gemv")
+def gemv(d_A: int, lda: int, d_x: int, d_y: int, m: int, k: int, stream=None, variant: int = 0,
+         exact: bool = False) -> None:
+    """y = A x on device pointers (the raw kernel: mvg_gemv, or mvg_gemv_exact)."""
+    if exact:
+        check(lib.mvg_gemv_exact_variant(d_A, lda, d_x, d_y, m, k, variant, stream), "mvg_gemv_exact")
+    else:
+        check(lib.mvg_gemv_variant(d_A, lda, d_x, d_y, m, k, variant, stream), "mvg_gemv")
 
 
 def multiply_multi(A: np.ndarray, X: np.ndarray) -> np.ndarray:
@@ -157,9 +162,10 @@ def multiply_multi(A: np.ndarray, X: np.ndarray) -> np.ndarray:
             b.free()
 
 
-def multiply_std_rowwise(A: np.ndarray, x: np.ndarray, variant: int = 0) -> np.ndarray:
+def multiply_std_rowwise(A: np.ndarray, x: np.ndarray, variant: int = 0, exact: bool = False) -> np.ndarray:
     """src/matr_utils.c:86-96 on the GPU: copies A, x to the current device, runs the HIP
-    GEMV, returns y. Matches the reference's sequential sum to <= 1e-12 relative."""
+    GEMV, returns y. Matches the reference's sequential sum to <= 1e-12 relative; with
+    exact=True (mvg_gemv_exact) bit for bit."""
     A = np.ascontiguousarray(A, dtype=np.float64)
     x = np.ascontiguousarray(x, dtype=np.float64)
     R, Cn = A.shape
@@ -167,7 +173,7 @@ def multiply_std_rowwise(A: np.ndarray, x: np.ndarray, variant: int = 0) -> np.n
         raise ValueError(f"x has shape {x.shape}, A has {Cn} columns")
     dA, dx, dy = DeviceBuffer(R * Cn).upload(A), DeviceBuffer(Cn).upload(x), DeviceBuffer(R)
     try:
-        gemv(dA.ptr, Cn, dx.ptr, dy.ptr, R, Cn, None, variant)
+        gemv(dA.ptr, Cn, dx.ptr, dy.ptr, R, Cn, None, variant, exact)
         check(lib.mvg_stream_sync(None), "sync")
         return dy.download(R)
     finally:
@@ -251,15 +257,18 @@ class KernelTiming:
 class Multiplier:
     """One distributed multiplier (alg, R x C) over a Comm. The drivers' loop body
     (distribute_data -> local product -> gather/reduce, e.g. multiplier_rowwise.c:139-141)
-    maps to distribute() -> multiply() -> collect()."""
+    maps to distribute() -> multiply() -> collect(). exact=True: y bit-identical to the
+    reference's (mvg_engine_set_exact); None leaves the MVG_EXACT environment default."""
 
-    def __init__(self, alg, R: int, Cn: int, comm: Comm):
+    def __init__(self, alg, R: int, Cn: int, comm: Comm, exact: bool | None = None):
         self.alg = _alg_id(alg)
         self.R, self.C = int(R), int(Cn)
         self.comm = comm
         h = C.c_void_p()
         check(lib.mvg_engine_create(C.byref(h), self.alg, self.R, self.C, comm.handle), "mvg_engine_create")
         self.handle = h.value
+        if exact is not None:
+            self.set_exact(exact)
         n = C.c_int()
         check(lib.mvg_comm_local_count(comm.handle, C.byref(n)), "mvg_comm_local_count")
         self.nlocal = n.value
@@ -314,6 +323,15 @@ class Multiplier:
         y = np.empty(max(self.R, 1), dtype=np.float64)
         check(lib.mvg_engine_collect(self.handle, y.ctypes.data), "mvg_engine_collect")
         return y[: self.R]
+
+    def set_exact(self, on: bool) -> None:
+        check(lib.mvg_engine_set_exact(self.handle, int(bool(on))), "mvg_engine_set_exact")
+
+    @property
+    def exact(self) -> bool:
+        v = C.c_int()
+        check(lib.mvg_engine_exact(self.handle, C.byref(v)), "mvg_engine_exact")
+        return bool(v.value)
 
     def kernel_timing(self, every: int) -> None:
         """Bracket every `every`-th multiply's GEMV with HIP events (0 = off)."""

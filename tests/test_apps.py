@@ -188,6 +188,23 @@ def test_mpiexec_multi_rank_matches_reference(tmp_path, golden, alg, P, dist):
     assert re.fullmatch(rf"480, 480, {P}, \d+\.\d{{6}}", lines[1]), lines
 
 
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,P", [("rowwise", 3), ("colwise", 4), ("colwise", 3), ("blockwise", 4),
+                                   ("blockwise", 2)])
+def test_mpiexec_exact_mode_writes_the_references_y_file(tmp_path, golden, alg, P):
+    # MVG_EXACT=1: P ranks (all on GPU 0), bit-exact kernels and the reference's combine order;
+    # the y file is then the reference's own y dump (oracle/ref_dump.h, "%.17g" per line) byte
+    # for byte — the block split at grids of at most two columns, where its sum is deterministic
+    (tmp_path / "data" / "out").mkdir(parents=True)
+    yout = tmp_path / "y.txt"
+    r = mpirun(alg, P, [480, 480], tmp_path, MVG_SYNTH=1, MVG_SAME_DEVICE=1, MVG_EXACT=1, MVG_ITERS=3,
+               MVG_Y_OUT=yout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = "".join("%.17g\n" % v for v in golden[f"sq_480/{alg}/P{P}"])
+    assert yout.read_text() == want
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_one_device(tmp_path):
     """bench.py's N > 1 path (the driver's scaling runs) at N = 2 under torch.distributed.run,

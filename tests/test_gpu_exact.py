@@ -1,0 +1,187 @@
+"""Bit-exact mode (mvg_gemv_exact, mvg_engine_set_exact): y identical to the reference's, not
+just within 1e-12.
+
+The reference's row sum is a sequential chain of rounded multiplies and rounded adds
+(src/matr_utils.c:87-93), its column split combines strips with MPICH's binomial MPI_Reduce
+(colwise.c:124) and its block split adds the grid row's partials into a zeroed y
+(blockwise.c:150-207). The exact kernels reproduce all of it, so every comparison here is
+np.array_equal — against the oracle (the pinned C restatement) on the same inputs, and against
+the golden y the real reference wrote (tests/golden), wherever the reference is deterministic
+(block split with more than two grid columns adds in message-arrival order; there the check is
+against the oracle's rank order, and within the tolerance against the reference).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import case_inputs, golden_runs, max_rel
+from matvec_mpi_multiplier_amd import _lib
+from matvec_mpi_multiplier_amd import multiplier as mm
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1, 1), (1, 2), (3, 5), (4, 8), (5, 7), (63, 129), (64, 128), (65, 127), (257, 1000), (1000, 257),
+          (33, 4096), (7, 20001), (2049, 512), (100, 1), (100, 2), (100, 3), (130, 16388), (3, 65538),
+          (200, 96), (129, 32), (64, 33), (700, 2080)]
+
+
+def signed(A, seed):
+    """Mixed-sign inputs: bit-exactness does not depend on the data being non-negative."""
+    rng = np.random.default_rng(seed)
+    return A * rng.choice([-1.0, 1.0], size=A.shape)
+
+
+def exact_variants():
+    lib = _lib.lib
+    return [(v, lib.mvg_gemv_exact_variant_name(v).decode()) for v in range(lib.mvg_gemv_exact_variant_count())]
+
+
+@pytest.mark.parametrize("m,k", SHAPES)
+def test_gemv_exact_every_variant_is_the_reference_sum(m, k):
+    A = signed(oracle.synth(m, k, 42), m * 7 + k)
+    x = signed(oracle.synth(1, k, 4242)[0], k)
+    want = oracle.multiply_std_rowwise(A, x)
+    for v, name in exact_variants():
+        if name.startswith("seq_r") and k % 2:
+            with pytest.raises(_lib.MvgError):
+                mm.multiply_std_rowwise(A, x, variant=v, exact=True)
+            continue
+        y = mm.multiply_std_rowwise(A, x, variant=v, exact=True)
+        assert np.array_equal(y, want), (name, m, k, max_rel(y, want))
+
+
+def test_gemv_exact_padded_lda_misaligned_and_k_zero():
+    m, k, lda = 130, 300, 512
+    full = oracle.synth(m, lda, 42)
+    x = oracle.synth(1, k + 1, 4242)[0]
+    dA, dx, dy = mm.DeviceBuffer(m * lda).upload(full), mm.DeviceBuffer(k + 1).upload(x), mm.DeviceBuffer(m)
+    want = oracle.multiply_std_rowwise(full[:, :k], x[:k])
+    for v, name in exact_variants():
+        mm.gemv(dA.ptr, lda, dx.ptr, dy.ptr, m, k, None, v, exact=True)
+        _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
+        assert np.array_equal(dy.download(), want), name
+    # A and x 8 bytes off a 16-B boundary: the automatic choice takes the 8-B path
+    want = oracle.multiply_std_rowwise(full[:, 1:k + 1], x[1:k + 1])
+    mm.gemv(dA.ptr + 8, lda, dx.ptr + 8, dy.ptr, m, k, None, 0, exact=True)
+    _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
+    assert np.array_equal(dy.download(), want)
+    with pytest.raises(_lib.MvgError):  # an LDS-DMA variant refuses the misaligned operands
+        mm.gemv(dA.ptr + 8, lda, dx.ptr + 8, dy.ptr, m, k, None, 2, exact=True)
+    dy.upload(np.full(m, 7.0))
+    mm.gemv(dA.ptr, lda, dx.ptr, dy.ptr, m, 0, None, 0, exact=True)
+    _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
+    assert np.array_equal(dy.download(), np.zeros(m))  # the reference's `sum = 0`
+
+
+def test_gemv_exact_reference_fixture_digits():
+    # data/matrix_4_8.txt x data/vector_8.txt: the reference's y printed with %.17g
+    from conftest import GOLDEN_DIR
+
+    A = np.loadtxt(os.path.join(GOLDEN_DIR, "matrix_4_8.txt")).reshape(4, 8)
+    x = np.loadtxt(os.path.join(GOLDEN_DIR, "vector_8.txt")).reshape(8)
+    y = mm.multiply_std_rowwise(A, x, exact=True)
+    assert ["%.17g" % v for v in y] == ["222.19999999999999", "196.55000000000001", "191.56999999999999",
+                                        "232.90000000000001"]
+
+
+@pytest.mark.parametrize("m,k", [(16384, 16384), (4096, 65536), (262144, 512)])
+def test_gemv_exact_full_width_rows_sampled(m, k):
+    """Large shapes on device-resident synthetic data: sampled rows against the oracle, bit for
+    bit, and run-to-run identity."""
+    s = None
+    dA, dx, dy = mm.DeviceBuffer(m * k), mm.DeviceBuffer(k), mm.DeviceBuffer(m)
+    _lib.check(_lib.lib.mvg_synth_fill_device(dA.ptr, k, m, k, 0, 0, k, 42, s), "fill")
+    _lib.check(_lib.lib.mvg_synth_fill_device(dx.ptr, k, 1, k, 0, 0, k, 4242, s), "fill")
+    mm.gemv(dA.ptr, k, dx.ptr, dy.ptr, m, k, s, 0, exact=True)
+    _lib.check(_lib.lib.mvg_stream_sync(s), "sync")
+    y = dy.download()
+    rows = np.unique(np.r_[0, 1, 63, 64, m // 2, m - 2, m - 1, np.random.default_rng(0).integers(0, m, 24)])
+    x = oracle.synth(1, k, 4242)[0]
+    for r in rows:
+        Ar = oracle.synth_block(int(r), 1, 0, k, k, 42)
+        assert oracle.multiply_std_rowwise(Ar, x)[0] == y[r], r
+    mm.gemv(dA.ptr, k, dx.ptr, dy.ptr, m, k, s, 0, exact=True)
+    _lib.check(_lib.lib.mvg_stream_sync(s), "sync")
+    assert np.array_equal(dy.download(), y)
+
+
+# ---------------------------------------------------------------- the engine in exact mode
+@pytest.fixture(scope="module")
+def comm1():
+    c = mm.Comm.init_all([0])
+    yield c
+    c.destroy()
+
+
+def test_engine_exact_p1_equals_every_golden_p1(comm1, golden, manifest):
+    for case, alg, p in golden_runs(manifest):
+        if p != 1 or case["R"] * case["C"] > 50_000_000:
+            continue
+        A, x = case_inputs(case)
+        with mm.Multiplier(alg, case["R"], case["C"], comm1, exact=True) as e:
+            assert e.exact
+            e.distribute(A, x)
+            e.multiply()
+            y = e.collect()
+        assert np.array_equal(y, golden[f"{case['name']}/{alg}/P1"]), (case["name"], alg)
+
+
+@pytest.mark.parametrize("alg", ["rowwise", "colwise", "blockwise"])
+def test_engine_exact_forced_collectives_p1(alg, monkeypatch, golden):
+    # the exact exchange (ncclGather of the partials + the combine kernel on rank 0) at world
+    # size 1, with the ring of partial buffers wrapping around
+    monkeypatch.setenv("MVG_ALWAYS_COLLECT", "1")
+    monkeypatch.setenv("MVG_EXACT", "1")
+    A, x = oracle.synth(480, 480, 42), oracle.synth(1, 480, 4242)[0]
+    c = mm.Comm.init_all([0])
+    try:
+        with mm.Multiplier(alg, 480, 480, c) as e:
+            assert e.exact
+            e.distribute(A, x)
+            for _ in range(11):
+                e.multiply()
+            y = e.collect()
+    finally:
+        c.destroy()
+    assert np.array_equal(y, golden[f"sq_480/{alg}/P1"])
+
+
+def test_engine_exact_shard_products_and_combines_at_p_gt_1(golden, manifest):
+    """P > 1 on one GPU: every rank's shard product with mvg_gemv_exact, combined in the
+    reference's order (the engine's combine kernels' order, restated on the host) — against the
+    golden y of the real reference at the same P, bit for bit where the reference is
+    deterministic."""
+    for case, alg, p in golden_runs(manifest):
+        if p == 1 or case["R"] * case["C"] > 50_000_000:
+            continue
+        A, x = case_inputs(case)
+        R, C = case["R"], case["C"]
+        parts = []
+        for r in range(p):
+            sh = mm.plan_shard(alg, R, C, p, r)
+            blk = np.ascontiguousarray(A[sh.row_off:sh.row_off + sh.n_rows, sh.col_off:sh.col_off + sh.n_cols])
+            parts.append(mm.multiply_std_rowwise(blk, x[sh.col_off:sh.col_off + sh.n_cols], exact=True))
+        if alg == "rowwise":
+            y = np.concatenate(parts)
+        elif alg == "colwise":
+            bufs = [q.copy() for q in parts]
+            mask = 1
+            while mask < p:
+                for r in range(0, p - mask, 2 * mask):
+                    bufs[r] = bufs[r] + bufs[r + mask]
+                mask *= 2
+            y = bufs[0]
+        else:
+            gr, gc = mm.get_2_most_closest_multipliers(p)
+            y = np.zeros(R)
+            lr = R // gr
+            for r in range(p):
+                y[(r // gc) * lr:(r // gc + 1) * lr] += parts[r]
+        key = f"{case['name']}/{alg}/P{p}"
+        if alg == "blockwise" and mm.get_2_most_closest_multipliers(p)[1] > 2:
+            assert np.array_equal(y, oracle.multiply(alg, A, x, p)), key
+            assert max_rel(y, golden[key]) <= 1e-12, key
+        else:
+            assert np.array_equal(y, golden[key]), key

@@ -1,0 +1,80 @@
+"""Bit-exact GEMV variants (mvg_gemv_exact_variant) against the tree-summed auto GEMV, one
+MI355X (development tool, not part of the product).
+
+    python tools/sweep_exact.py [rounds] [shape,shape,...]
+
+Times every exact variant and the default mvg_gemv on each shape with HIP events (interleaved
+rounds, 10 launches per timing), checks that the exact result agrees with the tree-summed one to
+1e-12 and is identical run to run, and prints one JSON object per (shape, variant).
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
+
+SHAPES = [
+    ("cfg2_16384sq", 16384, 16384),
+    ("cfg5_shard_524288x512", 524288, 512),
+    ("cfg3_g8_strip_65536x8192", 65536, 8192),
+    ("cfg4_block_65536x32768", 65536, 32768),
+    ("cfg5_full_4194304x512", 4194304, 512),
+    ("cfg3_g1_65536sq", 65536, 65536),
+    ("mid_32768x16384", 32768, 16384),
+    ("ref_4200sq", 4200, 4200),
+    ("ref_10200sq", 10200, 10200),
+]
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+    shapes = [s for s in SHAPES if not only or s[0] in only]
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    buf = torch.empty(max(m * k for _, m, k in shapes), dtype=torch.float64, device=dev)
+    xbuf = torch.empty(max(k for _, _, k in shapes), dtype=torch.float64, device=dev)
+    nvar = lib.mvg_gemv_exact_variant_count()
+    for name, M, K in shapes:
+        A = buf[: M * K].view(M, K)
+        x = xbuf[:K]
+        check(lib.mvg_synth_fill_device(A.data_ptr(), K, M, K, 0, 0, K, 42, s), "fill A")
+        check(lib.mvg_synth_fill_device(x.data_ptr(), K, 1, K, 0, 0, K, 4242, s), "fill x")
+        ref = torch.empty(M, dtype=torch.float64, device=dev)
+        check(lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), ref.data_ptr(), M, K, s), "gemv")
+        nbytes = 8 * (M * K + K + M)
+        runs = {"tree": lambda y: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)}
+        for v in range(nvar):
+            runs[lib.mvg_gemv_exact_variant_name(v).decode()] = (
+                lambda y, v=v: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, v, s))
+        res = {}
+        y = torch.empty(M, dtype=torch.float64, device=dev)
+        for key, fn in runs.items():
+            check(fn(y), key)
+            y1 = y.clone()
+            check(fn(y), key)
+            res[key] = {"ms": [], "rel": ((y - ref).abs() / ref.abs().clamp_min(1e-300)).max().item(),
+                        "deterministic": bool(torch.equal(y, y1))}
+        for _ in range(rounds):
+            for key, fn in runs.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                check(fn(y), key)
+                e0.record()
+                for _ in range(10):
+                    fn(y)
+                e1.record()
+                e1.synchronize()
+                res[key]["ms"].append(e0.elapsed_time(e1) / 10)
+        for key, r in res.items():
+            ms = sorted(r["ms"])
+            med = ms[len(ms) // 2]
+            print(json.dumps({"shape": name, "M": M, "K": K, "variant": key, "median_us": round(med * 1e3, 2),
+                              "min_us": round(ms[0] * 1e3, 2), "GBps_median": round(nbytes / (med * 1e-3) / 1e9, 1),
+                              "max_rel_vs_tree": r["rel"], "deterministic": r["deterministic"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
