@@ -182,3 +182,63 @@ def test_shared_host_matrix_two_ranks(stale):
         assert p.exitcode == 0
     assert got == [(0, "ok"), (1, "ok")]
     assert not os.path.exists(f"/dev/shm/mvg_test_{port}")
+
+
+def _exact_worker(rank, world, port, case, R, C, alg, outq):
+    """The exact-mode exchange (engine.cpp exchange_exact) over gloo: every rank's partial
+    gathered to rank 0 in rank order, then added there in the reference's order — MPICH's
+    binomial MPI_Reduce for the column split, the grid row's partials into a zeroed y in rank
+    order for the block split (the order of the combine kernels in csrc/gemv_exact.hip)."""
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd import multiplier as mm
+    from oracle import oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        A, x = _inputs(case, R, C)
+        s = mm.plan_shard(alg, R, C, world, rank)
+        blk = A[s.row_off:s.row_off + s.n_rows, s.col_off:s.col_off + s.n_cols]
+        part = torch.from_numpy(oracle.multiply_std_rowwise(blk, x[s.col_off:s.col_off + s.n_cols]).copy())
+        gl = [torch.empty_like(part) for _ in range(world)] if rank == 0 else None
+        dist.gather(part, gather_list=gl, dst=0)
+        if rank == 0:
+            parts = [g.numpy().copy() for g in gl]
+            if alg == "colwise":
+                mask = 1
+                while mask < world:
+                    for r in range(0, world - mask, 2 * mask):
+                        parts[r] = parts[r] + parts[r + mask]
+                    mask *= 2
+                y = parts[0]
+            else:
+                gr, gc = mm.get_2_most_closest_multipliers(world)
+                lr = R // gr
+                y = np.zeros(R)
+                for r in range(world):
+                    y[(r // gc) * lr:(r // gc + 1) * lr] = y[(r // gc) * lr:(r // gc + 1) * lr] + parts[r]
+            outq.put(y)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,R,C,alg,P", [("fixture_4x8", 4, 8, "colwise", 4), ("sq_480", 480, 480, "colwise", 4),
+                                            ("sq_480", 480, 480, "colwise", 3), ("sq_480", 480, 480, "blockwise", 4),
+                                            ("wide_120x6000", 120, 6000, "blockwise", 2)])
+def test_gloo_exact_exchange_is_bit_identical_to_reference(golden, case, R, C, alg, P):
+    # where the RCCL/gloo reduce differs from MPICH in the last bit (the replay above at P = 4),
+    # the exact exchange gives the reference's own bits
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exact_worker, args=(r, P, port, case, R, C, alg, q)) for r in range(P)]
+    for p in procs:
+        p.start()
+    y = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(y, golden[f"{case}/{alg}/P{P}"])
