@@ -268,7 +268,11 @@ class Multiplier:
         check(lib.mvg_engine_create(C.byref(h), self.alg, self.R, self.C, comm.handle), "mvg_engine_create")
         self.handle = h.value
         if exact is not None:
-            self.set_exact(exact)
+            try:
+                self.set_exact(exact)
+            except Exception:
+                self.destroy()
+                raise
         n = C.c_int()
         check(lib.mvg_comm_local_count(comm.handle, C.byref(n)), "mvg_comm_local_count")
         self.nlocal = n.value
