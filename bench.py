@@ -18,7 +18,8 @@ restatement of its MPI loop on the full matrix beside it; the restatement alone 
 reference cannot run), `end_to_end` (distribution from the root's host memory + multiply + y on
 the root, the reference's timing semantics), and `configs`: BASELINE.json configs 3-5 at their
 own fixed sizes on the same N GPUs (strong scaling, device-resident, same engine, same step),
-so one scaling run covers every multi-GPU config; supplementary, never `value`. `exact`: the
+so one scaling run covers every multi-GPU config (each also in bit-exact mode, `configs[].exact`);
+supplementary, never `value`. `exact`: the
 same workload with the engine in bit-exact mode (mvg_engine_set_exact: y identical to the
 reference's sequential sums), its step rate and kernel roofline fraction, and (rank 0, N = 1,
 row split) its y compared bit for bit with the oracle port's and the real reference's.
@@ -323,7 +324,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
     for name, alg, R, C in (by_num[int(k)] for k in args.configs.split(",") if k.strip()):
         sh = mm.plan_shard(alg, R, C, n, rank)
         part = R if alg == "colwise" else sh.y_len
-        need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + 9 * part + R) + (1 << 30)
+        need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + (9 + n) * part + R) + (1 << 30)  # + exact-mode gather buffer
         free = torch.cuda.mem_get_info(local)[0]
         ok = torch.tensor([1.0 if free >= need else 0.0], dtype=torch.float64, device=f"cuda:{local}")
         if distributed:
@@ -331,16 +332,11 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
         if float(ok[0]) < 1.0:
             out.append({"config": name, "alg": alg, "R": R, "C": C, "skipped": f"needs {need >> 30} GiB of HBM per GPU"})
             continue
-        e = mm.Multiplier(alg, R, C, comm)
-        try:
-            e.fill_synth()
-            for _ in range(3):
-                e.multiply()
-            e.sync()
+        def timed(e, steps):
             e.kernel_timing(args.event_every)
             barrier()
             t0 = time.perf_counter()
-            for _ in range(args.config_steps):
+            for _ in range(steps):
                 e.multiply()
             e.sync()
             barrier()
@@ -350,15 +346,42 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             t = torch.tensor([el, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
             if distributed:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el, kms = float(t[0]), float(t[1])
-            y = e.collect()
-            if rank == 0:
-                assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range"
-        finally:
-            e.destroy()
+            return float(t[0]), float(t[1])
+
         total = sum(8 * (s.n_rows * s.n_cols + s.n_cols + (R if alg == "colwise" else s.y_len))
                     for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
         per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
+        exact = None
+        e = mm.Multiplier(alg, R, C, comm)
+        try:
+            e.fill_synth()
+            for _ in range(3):
+                e.multiply()
+            e.sync()
+            el, kms = timed(e, args.config_steps)
+            y = e.collect()
+            if rank == 0:
+                assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range"
+            if not args.no_exact:
+                # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
+                # every partial to rank 0, the reference's combine order there)
+                e.set_exact(True)
+                for _ in range(2):
+                    e.multiply()
+                e.sync()
+                xsteps = max(5, args.config_steps // 2)
+                xel, xkms = timed(e, xsteps)
+                yx = e.collect()
+                e.set_exact(False)
+                exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
+                         "steps": xsteps, "kernel": exact_kernel_name(sh), "kernel_ms": round(xkms, 5),
+                         "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
+                if rank == 0:
+                    rel = float(np.max(np.abs(yx - y) / np.abs(y)))
+                    assert rel <= 1e-12, f"{name}: exact y differs from the tree-summed y by {rel}"
+                    exact["max_rel_vs_tree"] = rel
+        finally:
+            e.destroy()
         gr, gc = mm.get_2_most_closest_multipliers(n)
         out.append({
             "config": name, "alg": alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
@@ -367,6 +390,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             "ms_per_step": round(el / args.config_steps * 1e3, 4), "steps": args.config_steps,
             "kernel": kernel_name(sh), "kernel_ms": round(kms, 5),
             "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
+            "exact": exact,
         })
     return out
 
