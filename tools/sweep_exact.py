@@ -26,6 +26,10 @@ SHAPES = [
     ("mid_32768x16384", 32768, 16384),
     ("ref_4200sq", 4200, 4200),
     ("ref_10200sq", 10200, 10200),
+    ("cfg4_full_131072sq", 131072, 131072),
+    ("tall_131072x16384", 131072, 16384),
+    ("tall_262144x8192", 262144, 8192),
+    ("tall_1048576x2048", 1048576, 2048),
 ]
 
 
