@@ -10,10 +10,10 @@
 //
 // A sequential chain cannot be split over lanes, so one lane owns one row for the whole of K.
 // Reading A that way directly (64 lanes -> 64 rows per load instruction) would defeat
-// coalescing; instead each one-wave workgroup owns 64 consecutive rows and streams them through
-// LDS in tiles of 64 rows x 2T columns:
-//   load  : T `global_load_lds_dwordx4` per tile (LDS-DMA, no VGPRs, nt): instruction i fills
-//           rows [i*64/T, +64/T) of the tile, every row segment a contiguous 16*T bytes of A;
+// coalescing; instead each one-wave workgroup owns RW consecutive rows (16, 32 or 64) and streams
+// them through LDS in tiles of RW rows x 2T columns:
+//   load  : RW*T/64 `global_load_lds_dwordx4` per tile (LDS-DMA, no VGPRs, nt): instruction i
+//           fills rows [i*64/T, +64/T) of the tile, every row segment a contiguous 16*T bytes;
 //   read  : lane l takes row l's 16-B chunks in column order with `ds_read_b128`;
 //   swizzle: a lane-linear LDS image would put chunk k of all 64 rows in the same bank group,
 //           so the source address of LDS slot s in row r is chunk s ^ (r & 15) and the read of
@@ -22,7 +22,9 @@
 //   x     : the tile's x values are wave-uniform, read through the scalar cache into SGPRs and
 //           used as v_mul_f64 operands;
 //   pipeline: NB tile buffers per wave, NB-1 tiles' loads in flight behind the one being summed,
-//           retired with a counted `s_waitcnt vmcnt(T*(NB-1))` (hipcc does not track LDS-DMA).
+//           retired with a counted `s_waitcnt vmcnt(RW*T/64*(NB-1))` (hipcc does not track
+//           LDS-DMA completion: it emits no wait before a ds_read of a DMA'd buffer).
+// With RW < 64 the upper lanes repeat rows and store nothing (more waves for few rows).
 // Rows past M re-read row M-1 (never stored); the column tail K % 2T and any A that is not
 // 16-B aligned with an even lda take per-lane 8-B loads in the same column order.
 #include "common.h"
@@ -40,8 +42,7 @@ typedef __attribute__((address_space(1))) void* gbl_void_t;
 // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8]; the
 // others left at "no wait"), fenced against compiler reordering of memory operations: the
 // LDS-DMA writes of the tile about to be read are complete once at most N vector-memory
-// operations of this wave are outstanding. (The builtin rather than inline asm: a kernel with
-// inline asm is assumed to use every AGPR, which halves occupancy.)
+// operations of this wave are outstanding.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx950");
