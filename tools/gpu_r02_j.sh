@@ -1,0 +1,12 @@
+# Round 2, call J: what the driver runs at round end — pytest -m gpu, smoke(), default bench.
+set -o pipefail
+mkdir -p gpurun_out/r02j
+O=gpurun_out/r02j
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+tail -2 $O/pytest_gpu.log
+[ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/pytest_gpu.log | head -20; exit $rc; }
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+cat $O/smoke.log
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['roofline'], d['exact'], d['cpu_baseline']['value'], d['cpu_baseline']['port']['value'])"
+echo all-done
