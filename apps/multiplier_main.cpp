@@ -25,6 +25,7 @@
 //   MVG_Y_OUT=path     write y, "%.17g" per line (the reference never writes y)
 //   MVG_EXACT=1        bit-exact mode (mvg_engine_set_exact): y, and so the MVG_Y_OUT file, is
 //                      identical to the reference's (its sequential sums and combine orders)
+//   MVG_OVERLAP=n      distribute A in n row chunks, each chunk's GEMV behind its copy
 //   MVG_DATA_DIR=dir   input directory (default ./data, matr_utils.c:45,68)
 //   MVG_ITER_LOG=path  write every timed iteration's end-to-end time (s), one per line
 // Besides the CSV it prints the device-resident time (GEMV + collective only, A resident).

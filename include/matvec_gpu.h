@@ -251,6 +251,13 @@ int mvg_engine_destroy(mvg_engine* e);
  * result for rank-order message arrival; its own order varies run to run). */
 int mvg_engine_set_exact(mvg_engine* e, int on);
 int mvg_engine_exact(const mvg_engine* e, int* on);
+/* Chunked distribution (off by default; MVG_OVERLAP=n in the environment sets it at creation):
+ * chunks > 1 makes distribute / distribute_shared move each shard's rows in that many chunks on
+ * a copy stream, and the next multiply runs each chunk's GEMV as soon as its rows have landed,
+ * so only the last chunk's GEMV follows the transfer (the root-send distribution of one process
+ * per GPU is unchanged). 0 or 1 = one copy, then the GEMV. y is the same either way (row chunks
+ * are independent products; bit for bit in exact mode). */
+int mvg_engine_set_overlap(mvg_engine* e, int chunks);
 
 /* ------------------------------------------------------------------ text I/O (src/matr_utils.c)
  * Same file names under the same directory convention: <dir>/matrix_<R>_<C>.txt,

@@ -135,6 +135,7 @@ SIGNATURES = {
     "mvg_engine_destroy": (C.c_int, [_p]),
     "mvg_engine_set_exact": (C.c_int, [_p, C.c_int]),
     "mvg_engine_exact": (C.c_int, [_p, C.POINTER(C.c_int)]),
+    "mvg_engine_set_overlap": (C.c_int, [_p, C.c_int]),
     "mvg_matrix_filename": (C.c_int, [_i64, _i64, C.c_char_p, C.c_size_t]),
     "mvg_vector_filename": (C.c_int, [_i64, C.c_char_p, C.c_size_t]),
     "mvg_load_matr": (C.c_int, [C.c_char_p, _i64, _i64, _p]),

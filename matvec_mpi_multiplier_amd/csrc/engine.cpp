@@ -84,6 +84,12 @@ struct Shard {
     double* dy_parts[kRing] = {};
     hipEvent_t gemv_done[kRing] = {};  // GEMV into dy_parts[b] finished
     hipEvent_t x_done[kRing] = {};     // exchange reading dy_parts[b] finished
+    // chunked distribution (mvg_engine_set_overlap): row chunk c of A landed (copy_stream); the
+    // next multiply runs the GEMV of chunk c behind it, while later chunks are still copying
+    std::vector<hipEvent_t> chunk_ev;
+    std::vector<int64_t> chunk_row;   // chunk c = rows [chunk_row[c], chunk_row[c + 1])
+    hipEvent_t copy_ready = nullptr;  // s.stream's work before the copies (the last GEMV reads dA)
+    bool chunks_pending = false;
     double* dy_row = nullptr;   // block-split row leader: reduced slice (lr doubles)
     double* dy = nullptr;       // rank 0: the full y (R doubles)
     double* stage[2] = {nullptr, nullptr};  // root: staging for root->peer sends (rank mode)
@@ -103,6 +109,7 @@ struct mvg_engine {
     bool always_collect = false;  // run the collectives even at nranks == 1 (tests)
     bool distributed = false;
     bool exact = false;         // bit-exact mode: mvg_gemv_exact + the reference's combine orders
+    int overlap_chunks = 0;     // > 1: distribute in row chunks, each chunk's GEMV behind its copy
     int timing_every = 0;       // record kernel events on every Nth multiply (0 = off)
     int64_t nx = 0;             // multiplies with an exchange issued so far
     bool x_pending = false;     // an exchange may still run (slot (nx - 1) % ring)
@@ -150,6 +157,8 @@ void free_shard(Shard& s) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
     }
+    for (hipEvent_t ev : s.chunk_ev) (void)hipEventDestroy(ev);
+    if (s.copy_ready) (void)hipEventDestroy(s.copy_ready);
     s.ev_pool.clear();
     for (int k = 0; k < MVG_MAX_XSTEPS; ++k)
         if (s.owns_xcomm[k] && s.xcomm[k]) (void)ncclCommDestroy(s.xcomm[k]);
@@ -179,16 +188,45 @@ inline int64_t x_off(const mvg_shard& p) { return p.col_off; }
 inline int64_t x_len(const mvg_shard& p) { return p.n_cols; }
 
 // Every local device pulls its own shard (and x segment) from host memory that holds the
-// whole A and x, over its own PCIe link, concurrently (one stream per device).
+// whole A and x, over its own PCIe link, concurrently (one stream per device). With
+// overlap_chunks > 1 the shard's rows go over in that many chunks on the copy stream, each
+// followed by an event, and the next multiply runs each chunk's GEMV as soon as the chunk has
+// landed: only the last chunk's GEMV is left after the transfer.
 int distribute_direct(mvg_engine* e, const double* A, const double* x) {
     const int64_t C = e->C;
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
         const mvg_shard& p = s.plan;
-        int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
+        const int nch = e->overlap_chunks > 1 && p.n_rows >= 2 * (int64_t)e->overlap_chunks ? e->overlap_chunks : 0;
+        s.chunks_pending = false;
+        if (nch == 0) {
+            int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
+            if (rc != MVG_OK) return rc;
+            rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
+            if (rc != MVG_OK) return rc;
+            continue;
+        }
+        if (!s.copy_ready) MVG_HIP(hipEventCreateWithFlags(&s.copy_ready, hipEventDisableTiming));
+        while ((int)s.chunk_ev.size() < nch) {
+            hipEvent_t ev;
+            MVG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            s.chunk_ev.push_back(ev);
+        }
+        // the copies overwrite dA and dx, which the GEMV last queued on s.stream still reads
+        MVG_HIP(hipEventRecord(s.copy_ready, s.stream));
+        MVG_HIP(hipStreamWaitEvent(s.copy_stream, s.copy_ready, 0));
+        int rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.copy_stream);
         if (rc != MVG_OK) return rc;
-        rc = h2d_region(s.dx, x + x_off(p), x_len(p), 1, x_len(p), s.stream);
-        if (rc != MVG_OK) return rc;
+        s.chunk_row.assign(nch + 1, 0);
+        for (int c = 0; c <= nch; ++c) s.chunk_row[c] = p.n_rows * c / nch;
+        for (int c = 0; c < nch; ++c) {
+            const int64_t r0 = s.chunk_row[c], r1 = s.chunk_row[c + 1];
+            rc = h2d_region(s.dA + r0 * p.n_cols, A + (p.row_off + r0) * C + p.col_off, C, r1 - r0, p.n_cols,
+                            s.copy_stream);
+            if (rc != MVG_OK) return rc;
+            MVG_HIP(hipEventRecord(s.chunk_ev[c], s.copy_stream));
+        }
+        s.chunks_pending = true;
     }
     return MVG_OK;
 }
@@ -366,6 +404,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
     if (const char* v = getenv("MVG_XRING")) e->ring = std::max(1, std::min(kRing, atoi(v)));
     const char* ex = getenv("MVG_EXACT");
     const bool want_exact = ex && ex[0] == '1';
+    if (const char* ov = getenv("MVG_OVERLAP")) e->overlap_chunks = std::max(0, atoi(ov));
 
     e->shards.resize(comm->locals.size());
     auto bail = [&](int code) {
@@ -507,6 +546,14 @@ int mvg_engine_exact(const mvg_engine* e, int* on) {
     return MVG_OK;
 }
 
+int mvg_engine_set_overlap(mvg_engine* e, int chunks) {
+    if (!e || chunks < 0) return fail(MVG_E_INVALID, "mvg_engine_set_overlap: bad arguments");
+    int rc = mvg_engine_sync(e);
+    if (rc != MVG_OK) return rc;
+    e->overlap_chunks = chunks;
+    return MVG_OK;
+}
+
 int mvg_engine_shard(const mvg_engine* e, int i, mvg_shard* out) {
     if (!e || !out || i < 0 || i >= (int)e->shards.size()) return fail(MVG_E_INVALID, "bad index");
     *out = e->shards[i].plan;
@@ -562,6 +609,7 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
         // exactly one local shard
         Shard& s = e->shards[0];
         MVG_HIP(hipSetDevice(s.device));
+        s.chunks_pending = false;  // the root-send form always lands whole shards on s.stream
         // the sends/recvs below use the world communicator on s.stream: order them after any
         // exchange still running on s.xstream (one communicator, one order of operations)
         if (e->x_pending) MVG_HIP(hipStreamWaitEvent(s.stream, s.x_done[(e->nx - 1) % e->ring], 0));
@@ -673,7 +721,9 @@ int mvg_engine_multiply(mvg_engine* e) {
     DeviceGuard g;
     const int nsteps = e->shards[0].nsteps;
     const bool solo = nsteps == 0;  // P == 1: the product goes straight into y
-    const bool timed = e->timing_every > 0 && (e->multiply_calls++ % e->timing_every) == 0;
+    bool chunked = false;  // a chunked distribution is pending: the GEMVs wait on copies, not timed
+    for (auto& s : e->shards) chunked |= s.chunks_pending;
+    const bool timed = e->timing_every > 0 && (e->multiply_calls++ % e->timing_every) == 0 && !chunked;
     const bool serial = e->ring == 1;
     const int b = solo ? 0 : (int)(e->nx % e->ring);
     // The GEMV writes dy_parts[b]; the exchange that last read it was multiply nx - ring's. The
@@ -702,8 +752,21 @@ int mvg_engine_multiply(mvg_engine* e) {
             ++s.ev_used;
             MVG_HIP(hipEventRecord(t0, s.stream));
         }
-        int rc = e->exact ? mvg_gemv_exact(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream)
-                          : mvg_gemv(s.dA, p.n_cols, s.dx, out, p.n_rows, p.n_cols, s.stream);
+        auto gemv = [&](int64_t r0, int64_t rows) {
+            return e->exact ? mvg_gemv_exact(s.dA + r0 * p.n_cols, p.n_cols, s.dx, out + r0, rows, p.n_cols, s.stream)
+                            : mvg_gemv(s.dA + r0 * p.n_cols, p.n_cols, s.dx, out + r0, rows, p.n_cols, s.stream);
+        };
+        int rc = MVG_OK;
+        if (s.chunks_pending) {
+            // row chunks are independent products: each runs once its rows have landed
+            for (size_t c = 0; c + 1 < s.chunk_row.size() && rc == MVG_OK; ++c) {
+                MVG_HIP(hipStreamWaitEvent(s.stream, s.chunk_ev[c], 0));
+                rc = gemv(s.chunk_row[c], s.chunk_row[c + 1] - s.chunk_row[c]);
+            }
+            s.chunks_pending = false;
+        } else {
+            rc = gemv(0, p.n_rows);
+        }
         if (rc != MVG_OK) return rc;
         if (timed) MVG_HIP(hipEventRecord(t1, s.stream));
         if (!solo && !serial) {

@@ -331,6 +331,10 @@ class Multiplier:
     def set_exact(self, on: bool) -> None:
         check(lib.mvg_engine_set_exact(self.handle, int(bool(on))), "mvg_engine_set_exact")
 
+    def set_overlap(self, chunks: int) -> None:
+        """Distribute in `chunks` row chunks, each chunk's GEMV behind its copy (0/1 = off)."""
+        check(lib.mvg_engine_set_overlap(self.handle, int(chunks)), "mvg_engine_set_overlap")
+
     @property
     def exact(self) -> bool:
         v = C.c_int()

@@ -380,3 +380,39 @@ def test_device_numa_node_and_first_touch():
     assert node.value >= -1
     a = np.full(10_000_000, 1.0)
     assert _lib.lib.mvg_host_first_touch(a.ctypes.data, a.nbytes, 0) == 0 and not a.any()
+
+
+# ---------------------------------------------------------------- chunked distribution overlap
+@pytest.mark.parametrize("alg", ["rowwise", "colwise", "blockwise"])
+@pytest.mark.parametrize("chunks", [2, 7])
+def test_overlapped_distribution_gives_the_same_y(comm1, alg, chunks):
+    """mvg_engine_set_overlap: the shard goes over in row chunks and each chunk's GEMV runs behind
+    its copy. Back-to-back distribute/multiply cycles with different inputs and no sync in
+    between (the copies must wait for the GEMV still reading the shard), tree and exact mode."""
+    R, C = 1000, 768
+    A1, A2 = oracle.synth(R, C, 42), oracle.synth(R, C, 7)
+    x1, x2 = oracle.synth(1, C, 4242)[0], oracle.synth(1, C, 99)[0]
+    for exact in (False, True):
+        with mm.Multiplier(alg, R, C, comm1, exact=exact) as e:
+            e.set_overlap(chunks)
+            ys = []
+            for A, x in ((A1, x1), (A2, x2), (A1, x2)):
+                e.distribute(A, x)
+                e.multiply()
+                ys.append(e.collect())
+            # no collect (no sync) between: the second copies must wait for the first GEMV
+            e.distribute(A1, x1)
+            e.multiply()
+            e.distribute(A2, x2)
+            e.multiply()
+            ys.append(e.collect())
+            e.set_overlap(0)
+            e.distribute(A2, x1)
+            e.multiply()
+            ys.append(e.collect())
+        for y, (A, x) in zip(ys, ((A1, x1), (A2, x2), (A1, x2), (A2, x2), (A2, x1))):
+            want = oracle.multiply(alg, A, x, 1)
+            if exact:
+                assert np.array_equal(y, want), (alg, chunks)
+            else:
+                assert max_rel(y, want) <= TOL, (alg, chunks)
