@@ -44,7 +44,7 @@ def test_gemv_exact_every_variant_is_the_reference_sum(m, k):
     x = signed(oracle.synth(1, k, 4242)[0], k)
     want = oracle.multiply_std_rowwise(A, x)
     for v, name in exact_variants():
-        if name.startswith("seq_r") and k % 2:
+        if name not in ("auto", "seq_scalar") and k % 2:  # the LDS-DMA forms need an even lda
             with pytest.raises(_lib.MvgError):
                 mm.multiply_std_rowwise(A, x, variant=v, exact=True)
             continue
