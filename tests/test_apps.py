@@ -99,6 +99,11 @@ def test_c_binding_example_runs_the_fixture(workdir, golden):
     y = np.array([float(v) for v in r.stdout.split()[-4:]])
     assert max_rel(y, golden["fixture_4x8/rowwise/P1"]) <= 1e-12
     assert re.fullmatch(r"4, 8, 1, \d+\.\d{6}\n", r.stderr.splitlines()[-1] + "\n")
+    # the same C program with MVG_EXACT=1: the reference's digits exactly
+    r = subprocess.run([os.path.join(REPO, "bin", "rowwise_binding"), "4", "8", "1"], cwd=workdir,
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, MVG_EXACT="1"))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split()[-4:] == ["%.17g" % v for v in golden["fixture_4x8/rowwise/P1"]]
 
 
 # ---- launched like the reference: mpiexec -n P bin/multiplier_<alg> R C (test.sh:11)
