@@ -541,11 +541,22 @@ def cpu_baseline(args, R, C, y_gpu, y_exact=None):
     if not ref_runner.available(args.alg) or not _splits(args.alg, rows, C, P):
         port["reference"] = "not run: oracle/_ref or mpiexec absent, or the sample does not split"
         return port
-    try:
-        r = ref_runner.run(args.alg, rows, C, P, timeout=args.ref_timeout, cpus=cpus)
-    except Exception as exc:  # the baseline must never sink the bench
-        port["reference"] = f"not run: {str(exc)[:300]}"
+    # the reference is communication-bound (its root scatters A through MPI shared memory every
+    # iteration): it runs once on the port's spread placement and once on consecutive cores, and
+    # the faster run is its baseline (both recorded)
+    from oracle import cpuset
+
+    runs = []
+    for label, cset in (("spread", cpus), ("compact", cpuset.pick_compact(P, gpu_numa_node()))):
+        try:
+            runs.append((label, cset, ref_runner.run(args.alg, rows, C, P, timeout=args.ref_timeout, cpus=cset)))
+        except Exception as exc:  # the baseline must never sink the bench
+            port.setdefault("reference_errors", []).append(f"{label}: {str(exc)[:200]}")
+    if not runs:
+        port["reference"] = "not run: " + "; ".join(port.get("reference_errors", []))
         return port
+    label, cpus, r = min(runs, key=lambda t: t[2]["seconds"])
+    placements = {lab: round(8 * (rows * C + C + rows) / rr["seconds"] / 1e9, 3) for lab, _, rr in runs}
     rel = float(np.max(np.abs(y_gpu[:rows] - r["y"]) / np.abs(r["y"])))
     assert rel <= 1e-12, f"GPU y differs from the reference's own y: {rel}"
     nbytes = 8 * (rows * C + C + rows)
@@ -555,7 +566,7 @@ def cpu_baseline(args, R, C, y_gpu, y_exact=None):
                       f"(oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its text inputs, its "
                       f"100-iteration loop (distribution from the root + sequential sums + collection); "
                       f"run {r['wall_s']:.1f} s incl. text loading; GPU y matches its y to {rel:.1e}",
-            "host_cpu": host_cpu(), "placement": port["placement"]["record"],
+            "host_cpu": host_cpu(), "placement": {**cpuset.describe(cpus), "kind": label, "GBps_by_placement": placements},
             "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")},
             "exact_vs_port": port.get("exact_vs_port"),
             **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}

@@ -79,6 +79,25 @@ def pick(n: int, numa_node: int | None = None) -> list[int]:
     return (_spread(first) + _spread(rest))[:max(1, n)]
 
 
+def pick_compact(n: int, numa_node: int | None = None) -> list[int]:
+    """n CPUs on consecutive physical cores (SMT siblings last), those of `numa_node` first: the
+    placement that suits a communication-bound run (MPI ranks exchanging through shared memory
+    stay on few L3 domains), where `pick` suits a bandwidth-bound one."""
+    allowed = sorted(os.sched_getaffinity(0))
+    node = _node_cpus(numa_node) if numa_node is not None else set()
+
+    def primary_first(cpus):
+        seen, first, later = set(), [], []
+        for c in cpus:
+            core = _cpu_key(c, "topology/thread_siblings_list")
+            (later if core in seen else first).append(c)
+            seen.add(core)
+        return first + later
+
+    first = primary_first([c for c in allowed if c in node])
+    return (first + primary_first([c for c in allowed if c not in node]))[:max(1, n)]
+
+
 @contextlib.contextmanager
 def confined(cpus: list[int]):
     """Confine this process (and the threads it starts meanwhile) to `cpus`; restore after."""
