@@ -30,6 +30,16 @@ SHAPES = [
     ("tall_131072x16384", 131072, 16384),
     ("tall_262144x8192", 262144, 8192),
     ("tall_1048576x2048", 1048576, 2048),
+    ("asym_1200x60000", 1200, 60000),
+    ("asym_120x60000", 120, 60000),
+    ("ref_600sq", 600, 600),
+    ("ref_1800sq", 1800, 1800),
+    ("mid_4096x16384", 4096, 16384),
+    ("mid_8192x16384", 8192, 16384),
+    ("mid_4096x32768", 4096, 32768),
+    ("mid_2048x65536", 2048, 65536),
+    ("mid_8192x8192", 8192, 8192),
+    ("mid_12288x12288", 12288, 12288),
 ]
 
 
