@@ -19,8 +19,10 @@
 //           so the source address of LDS slot s in row r is chunk s ^ (r & 15) and the read of
 //           chunk k goes to slot k ^ (l & 15) — the same involution on both sides, conflict-free
 //           over every ds_read_b128 lane group (rule 21 of the HIP guide);
-//   x     : the tile's x values are wave-uniform, read through the scalar cache into SGPRs and
-//           used as v_mul_f64 operands;
+//   x     : wave-uniform; gemv_seq reads it through the scalar cache into SGPRs (v_mul_f64
+//           operands), gemv_seq_x — the forms the dispatch uses — carries each tile's x segment
+//           in the same LDS ring and reads it back as a broadcast, so its latency stays off the
+//           sequential chain;
 //   pipeline: NB tile buffers per wave, NB-1 tiles' loads in flight behind the one being summed,
 //           retired with a counted `s_waitcnt vmcnt(RW*T/64*(NB-1))` (hipcc does not track
 //           LDS-DMA completion: it emits no wait before a ds_read of a DMA'd buffer).
@@ -150,6 +152,98 @@ __global__ __launch_bounds__(64) void gemv_seq(const double* __restrict__ A, int
     if (lane < RW && r0 + lane < M) y[r0 + lane] = sum;
 }
 
+// x through the LDS ring as well: each tile buffer carries the tile's x segment (one more
+// LDS-DMA instruction per tile, 1 KiB), read back with wave-uniform ds_read_b128 (a broadcast),
+// so x arrives with the tile instead of through scalar loads issued at the point of use (whose
+// L2 latency sat on the sequential chain). The LDS reads of chunk group g + 1 are issued before
+// the sums of group g (two register sets of G chunks), so the chain waits on neither.
+template <int RW, int T, int NB, int G>
+__global__ __launch_bounds__(64) void gemv_seq_x(const double* __restrict__ A, int64_t lda,
+                                                 const double* __restrict__ x,
+                                                 double* __restrict__ y, int64_t M, int64_t K) {
+    static_assert(RW == 16 || RW == 32 || RW == 64, "rows per wave");
+    static_assert(T >= 16 && T <= 64 && (T & (T - 1)) == 0, "tile width: 16..64 chunks");
+    static_assert(G >= 4 && T % G == 0, "chunk groups");
+    constexpr int kRows = 64 / T;
+    constexpr int kInst = RW / kRows + 1;  // + the x segment
+    static_assert(RW % kRows == 0, "a tile is whole instructions");
+    static_assert(NB >= 2 && kInst * (NB - 1) <= 63, "loads in flight must fit the vmcnt counter");
+    constexpr int kCols = 2 * T;
+    constexpr int kRowBytes = 16 * T;
+    constexpr int kTileBytes = RW * kRowBytes;
+    constexpr int kBufBytes = kTileBytes + 1024;  // tile + x segment (lanes past T repeat chunk T-1)
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NB * kBufBytes];
+
+    const int lane = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * RW;
+    const int64_t ntiles = K / kCols;
+    uint32_t off[kInst - 1];
+#pragma unroll
+    for (int i = 0; i < kInst - 1; ++i) {
+        const int row = i * kRows + lane / T;
+        const int64_t rr = r0 + row < M ? row : M - 1 - r0;
+        off[i] = (uint32_t)((rr * lda + 2 * ((lane % T) ^ (row & 15))) * (int64_t)sizeof(double));
+    }
+    const uint32_t xoff = (uint32_t)(2 * (lane < T ? lane : T - 1) * sizeof(double));
+    const unsigned char* const a0 = reinterpret_cast<const unsigned char*>(A + r0 * lda);
+    const unsigned char* const x0 = reinterpret_cast<const unsigned char*>(x);
+    auto issue = [&](int64_t t, int b) {
+        const int64_t colb = t * kCols * (int64_t)sizeof(double);
+#pragma unroll
+        for (int i = 0; i < kInst - 1; ++i)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(a0 + colb + off[i]),
+                                             (lds_void_t)(lds + b * kBufBytes + i * 1024), 16, 0, 2 /* nt */);
+        __builtin_amdgcn_global_load_lds((gbl_void_t)(x0 + colb + xoff), (lds_void_t)(lds + b * kBufBytes + kTileBytes),
+                                         16, 0, 0);
+    };
+
+    const int myr = lane % RW;
+    double sum = 0.0;
+    const uint32_t my_row = (uint32_t)(myr * kRowBytes + ((myr & 15) << 4));
+    auto consume = [&](int b) {
+        const unsigned char* tile = lds + b * kBufBytes;
+        const unsigned char* xs = tile + kTileBytes;
+        dbl2x a[2][G], xv[2][G];
+        auto read = [&](int g, dbl2x (&ad)[G], dbl2x (&xd)[G]) {
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                ad[k] = *reinterpret_cast<const dbl2x*>(tile + (my_row ^ (uint32_t)((g + k) << 4)));
+                xd[k] = *reinterpret_cast<const dbl2x*>(xs + (g + k) * 16);
+            }
+        };
+        read(0, a[0], xv[0]);
+#pragma unroll
+        for (int g = 0; g < T; g += G) {
+            const int cur = (g / G) & 1;
+            if (g + G < T) read(g + G, a[cur ^ 1], xv[cur ^ 1]);
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                sum = seq_step(sum, a[cur][k].x, xv[cur][k].x);
+                sum = seq_step(sum, a[cur][k].y, xv[cur][k].y);
+            }
+        }
+    };
+
+    for (int p = 0; p < NB - 1; ++p)
+        if (p < ntiles) issue(p, p);
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int64_t tn = t + NB - 1;
+        if (tn < ntiles) {
+            wait_lgkmcnt0();
+            issue(tn, (int)(tn % NB));
+            wait_vmcnt<kInst*(NB - 1)>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        consume((int)(t % NB));
+    }
+    int64_t rr = r0 + myr;
+    rr = rr < M ? rr : M - 1;
+    const double* arow = A + rr * lda;
+    for (int64_t j = ntiles * kCols; j < K; ++j) sum = seq_step(sum, arow[j], x[j]);
+    if (lane < RW && r0 + lane < M) y[r0 + lane] = sum;
+}
+
 // Any alignment, any lda: lane = row, 8-B loads walking the row (uncoalesced; small or odd
 // shapes only).
 __global__ __launch_bounds__(64) void gemv_seq_scalar(const double* __restrict__ A, int64_t lda,
@@ -231,17 +325,19 @@ struct SeqVariant {
 static constexpr SeqVariant kSeqVariants[] = {
     {"auto", nullptr, false, 64},          // 0
     {"seq_scalar", gemv_seq_scalar, false, 64},
+    // x through the scalar cache (the first form; kept for comparison)
     SEQ(64, 16, 2),   // LDS per wave: NB x RW x 16T bytes; 32 KiB
-    SEQ(64, 16, 3),   // 48 KiB
-    SEQ(64, 16, 4),   // 64 KiB
     SEQ(64, 32, 2),   // 64 KiB
     SEQ(32, 32, 2),   // 32 KiB
-    SEQ(32, 32, 3),   // 48 KiB
     SEQ(32, 64, 2),   // 64 KiB
     SEQ(16, 64, 2),   // 32 KiB
-    SEQ(16, 64, 3),   // 48 KiB
-    SEQ(16, 64, 4),   // 64 KiB
-    SEQ(16, 32, 4),   // 32 KiB
+    // x through the LDS ring, LDS reads one chunk group ahead of the sums
+    {"seqx_r32_t64_b2_g8", gemv_seq_x<32, 64, 2, 8>, true, 32},
+    {"seqx_r32_t64_b2_g16", gemv_seq_x<32, 64, 2, 16>, true, 32},
+    {"seqx_r64_t16_b2_g8", gemv_seq_x<64, 16, 2, 8>, true, 64},
+    {"seqx_r64_t32_b2_g8", gemv_seq_x<64, 32, 2, 8>, true, 64},
+    {"seqx_r16_t64_b2_g8", gemv_seq_x<16, 64, 2, 8>, true, 16},
+    {"seqx_r16_t32_b4_g8", gemv_seq_x<16, 32, 4, 8>, true, 16},
 };
 constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
 
@@ -258,24 +354,24 @@ constexpr int seq_id(const SeqVariant (&table)[N], const char* name) {
     return -1;
 }
 constexpr int kSeqScalar = seq_id(kSeqVariants, "seq_scalar");
-constexpr int kSeqR64T16 = seq_id(kSeqVariants, "seq_r64_t16_b2");
-constexpr int kSeqR64T32 = seq_id(kSeqVariants, "seq_r64_t32_b2");
-constexpr int kSeqR32T64 = seq_id(kSeqVariants, "seq_r32_t64_b2");
-constexpr int kSeqR16T64 = seq_id(kSeqVariants, "seq_r16_t64_b2");
+constexpr int kSeqShortRows = seq_id(kSeqVariants, "seqx_r64_t32_b2_g8");
+constexpr int kSeqManyRows = seq_id(kSeqVariants, "seqx_r64_t16_b2_g8");
+constexpr int kSeqDefault = seq_id(kSeqVariants, "seqx_r32_t64_b2_g16");
 static_assert(kSeqScalar > 0 && !kSeqVariants[kSeqScalar].vec, "8-B exact fallback");
-static_assert(kSeqR64T16 > 0 && kSeqR64T32 > 0 && kSeqR32T64 > 0 && kSeqR16T64 > 0,
-              "exact dispatch names a missing variant");
+static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqDefault > 0, "exact dispatch names a missing variant");
 
-// From the round-2 MI355X sweep (tools/sweep_exact.py -> profiles/r02/sweep_exact.jsonl). A lane
-// owns a row, so the row count sets the waves: with >= 65536 rows (>= 4 waves of 64 rows per
-// CU) 64-row waves with 256-B row segments per tile (7.0 TB/s at 65536^2 and 65536 x 32768,
-// 0.96-0.97 of the tree-summed kernel), 512-B segments when rows are short (K <= 1024: 4194304 x
-// 512 at 6.9 TB/s, level with the tree kernel on that box); 16384-65535 rows: 32-row waves with
-// 1-KiB segments (16384^2 at 6.5 TB/s); fewer: 16-row waves (the upper 48 lanes repeat rows).
+// From the round-2 MI355X sweeps (tools/sweep_exact.py -> profiles/r02/sweep_exact*.jsonl; the
+// last, sweep_exact7_x_lds.jsonl, over 11 shapes from 4200^2 to 65536^2 and 4194304 x 512). The
+// forms with x in the LDS ring and the LDS reads pipelined one chunk group ahead
+// (gemv_seq_x) beat the scalar-x forms wherever the chain, not HBM, was the limit (4096 x 16384:
+// 430 -> 185 us; 16384^2: 329 -> 323 us) and tie them at full occupancy. >= 65536 rows: 64-row
+// waves, 512-B row segments for short rows (K <= 1024: 4194304 x 512) and 256-B ones otherwise;
+// fewer rows: 32-row waves with 1-KiB segments, within 1.1x of the best form on every swept
+// shape below 65536 rows.
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     if (!seq_vec_ok(lda, aligned)) return kSeqScalar;
-    if (M >= 65536) return K <= 1024 ? kSeqR64T32 : kSeqR64T16;
-    return M >= 16384 ? kSeqR32T64 : kSeqR16T64;
+    if (M >= 65536) return K <= 1024 ? kSeqShortRows : kSeqManyRows;
+    return kSeqDefault;
 }
 
 }  // namespace mvg
