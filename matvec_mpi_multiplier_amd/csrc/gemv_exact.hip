@@ -29,6 +29,9 @@
 // With RW < 64 the upper lanes repeat rows and store nothing (more waves for few rows).
 // Rows past M re-read row M-1 (never stored); the column tail K % 2T and any A that is not
 // 16-B aligned with an even lda take per-lane 8-B loads in the same column order.
+// With fewer rows (< 12288) or very long ones (K >= 65536) the chain-hopping forms
+// (gemv_seq_hop, below) take over: L lanes share a row, the data arrives by plain coalesced
+// loads into VGPRs, and the running sum hops from lane to lane by DPP, still in column order.
 #include "common.h"
 
 // hipcc contracts a*b + c into an FMA by default (-ffp-contract=fast); the reference rounds the
@@ -244,6 +247,102 @@ __global__ __launch_bounds__(64) void gemv_seq_x(const double* __restrict__ A, i
     if (lane < RW && r0 + lane < M) y[r0 + lane] = sum;
 }
 
+// ------------------------------------------------------------------ chain hopping across lanes
+// The LDS forms above give every row one lane for the whole of K, so a wave advances one
+// element of each of its rows per step; where few rows exist (the reference's own R x 60000 and
+// 600^2 ... 10200^2 shapes) few waves run and each one's step rate — an add, a multiply, the LDS
+// reads and their waits — is the whole story. Here L lanes share a row instead: a segment of
+// L*W columns is one set of plain coalesced 16-B loads into VGPRs (lane c of the row's group
+// holds W consecutive columns), every lane forms its W products at once, and the chain walks the
+// group — lane c adds its W products in order, then the running sum hops to lane c+1 by DPP
+// (row_shr:1; wave_shr:1 beyond 16 lanes). Odd segments place the columns the other way round
+// (lane L-1-c holds the c-th W) and hop backwards, so each segment starts where the previous
+// one ended and the chain stays in column order without a wrap-around move. All lanes execute
+// every add; only the lane holding the chain adds its own products to the real sum, the others
+// carry garbage that the next hop overwrites. Per column: one dependent add plus 1/W of a hop.
+// U segments are in flight per wave (the compiler counts plain loads itself).
+template <int L, bool FWD>
+__device__ __forceinline__ double hop(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    constexpr int kCtrl = L <= 16 ? (FWD ? 0x111 : 0x101) : (FWD ? 0x138 : 0x130);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, kCtrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), kCtrl, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// One segment of the chain: lane t of the group adds its W products at step t, then hands over.
+template <int L, int W, bool FWD>
+__device__ __forceinline__ double hop_segment(double sum, const dbl2x (&a)[W / 2], const dbl2x (&xv)[W / 2]) {
+    double p[W];
+#pragma unroll
+    for (int v = 0; v < W / 2; ++v) p[2 * v] = a[v].x * xv[v].x, p[2 * v + 1] = a[v].y * xv[v].y;
+#pragma unroll
+    for (int t = 0; t < L; ++t) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) sum = sum + p[j];
+        if (t + 1 < L) sum = hop<L, FWD>(sum);
+    }
+    return sum;
+}
+
+template <int L, int W, int U>
+__global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A, int64_t lda,
+                                                   const double* __restrict__ x,
+                                                   double* __restrict__ y, int64_t M, int64_t K) {
+    static_assert(L == 1 || L == 2 || L == 4 || L == 8 || L == 16 || L == 32 || L == 64, "lanes per row");
+    static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B loads; segment pairs per unrolled step");
+    constexpr int R = 64 / L;  // rows per wave
+    constexpr int S = L * W;   // columns per segment
+    constexpr int V = W / 2;   // 16-B loads per lane per segment
+    const int lane = threadIdx.x;
+    const int c = lane % L;
+    const int64_t row = (int64_t)blockIdx.x * R + lane / L;
+    const int64_t rr = row < M ? row : M - 1;
+    const double* arow = A + rr * lda;
+    const int64_t nseg = K / S;
+    const int off[2] = {c * W, (L - 1 - c) * W};  // even / odd segment
+
+    double sum = 0.0;
+    if (nseg > 0) {
+        dbl2x a[U][V], xv[U][V];
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const int64_t s = i < nseg ? i : nseg - 1;
+            const dbl2x* pa = (const dbl2x*)(arow + s * S + off[i & 1]);
+            const dbl2x* px = (const dbl2x*)(x + s * S + off[i & 1]);
+#pragma unroll
+            for (int v = 0; v < V; ++v) a[i][v] = __builtin_nontemporal_load(pa + v), xv[i][v] = px[v];
+            __builtin_amdgcn_sched_barrier(0);  // same load order as the loop's refills
+        }
+        // Whole groups of U segments, one basic block: slot i is summed, then refilled U segments
+        // ahead; the scheduling barriers keep the loads in slot order, so the compiler's vmcnt
+        // waits retire exactly the slot about to be summed.
+        int64_t base = 0;
+        for (; base + U <= nseg; base += U) {
+#pragma unroll
+            for (int i = 0; i < U; ++i) {
+                sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
+                __builtin_amdgcn_sched_barrier(0);
+                const int64_t s = base + i + U < nseg ? base + i + U : nseg - 1;
+                const dbl2x* pa = (const dbl2x*)(arow + s * S + off[i & 1]);
+                const dbl2x* px = (const dbl2x*)(x + s * S + off[i & 1]);
+#pragma unroll
+                for (int v = 0; v < V; ++v) a[i][v] = __builtin_nontemporal_load(pa + v), xv[i][v] = px[v];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // the last nseg % U segments are already in slots 0 .. nseg % U - 1 (base is even)
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            if (base + i < nseg)
+                sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
+    }
+    // the chain ends in lane L-1 after an even-numbered last segment, in lane 0 otherwise
+    const int holder = (nseg & 1) ? L - 1 : 0;
+    for (int64_t j = nseg * S; j < K; ++j) sum = seq_step(sum, arow[j], x[j]);
+    if (c == holder && row < M) y[row] = sum;
+}
+
 // Any alignment, any lda: lane = row, 8-B loads walking the row (uncoalesced; small or odd
 // shapes only).
 __global__ __launch_bounds__(64) void gemv_seq_scalar(const double* __restrict__ A, int64_t lda,
@@ -317,11 +416,12 @@ typedef void (*seq_fn)(const double*, int64_t, const double*, double*, int64_t, 
 struct SeqVariant {
     const char* name;
     seq_fn fn;
-    bool vec;  // LDS-DMA path: needs 16-B aligned A, x and an even lda
+    bool vec;  // 16-B loads (LDS-DMA or plain): needs 16-B aligned A, x and an even lda
     int rows;  // rows per one-wave workgroup
 };
 
 #define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, true, RW}
+#define HOP(L, W, U) {"hop_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U>, true, 64 / L}
 static constexpr SeqVariant kSeqVariants[] = {
     {"auto", nullptr, false, 64},          // 0
     {"seq_scalar", gemv_seq_scalar, false, 64},
@@ -338,6 +438,19 @@ static constexpr SeqVariant kSeqVariants[] = {
     {"seqx_r64_t32_b2_g8", gemv_seq_x<64, 32, 2, 8>, true, 64},
     {"seqx_r16_t64_b2_g8", gemv_seq_x<16, 64, 2, 8>, true, 16},
     {"seqx_r16_t32_b4_g8", gemv_seq_x<16, 32, 4, 8>, true, 16},
+    // L lanes per row, the chain hopping across them (registers, no LDS)
+    HOP(64, 8, 4),
+    HOP(32, 8, 4),
+    HOP(32, 4, 8),
+    HOP(16, 8, 4),
+    HOP(16, 4, 8),
+    HOP(16, 2, 16),
+    HOP(8, 8, 4),
+    HOP(8, 4, 8),
+    HOP(8, 2, 16),
+    HOP(8, 2, 24),
+    HOP(4, 4, 8),
+    HOP(4, 2, 16),
 };
 constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
 
@@ -356,22 +469,33 @@ constexpr int seq_id(const SeqVariant (&table)[N], const char* name) {
 constexpr int kSeqScalar = seq_id(kSeqVariants, "seq_scalar");
 constexpr int kSeqShortRows = seq_id(kSeqVariants, "seqx_r64_t32_b2_g8");
 constexpr int kSeqManyRows = seq_id(kSeqVariants, "seqx_r64_t16_b2_g8");
-constexpr int kSeqDefault = seq_id(kSeqVariants, "seqx_r32_t64_b2_g16");
+constexpr int kSeqMidRows = seq_id(kSeqVariants, "seqx_r32_t64_b2_g16");
+constexpr int kHopRows = seq_id(kSeqVariants, "hop_l8_w2_u16");
+constexpr int kHopLongRows = seq_id(kSeqVariants, "hop_l8_w2_u24");
+constexpr int kHopWide = seq_id(kSeqVariants, "hop_l16_w4_u8");
+constexpr int kHopFewRows = seq_id(kSeqVariants, "hop_l32_w8_u4");
 static_assert(kSeqScalar > 0 && !kSeqVariants[kSeqScalar].vec, "8-B exact fallback");
-static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqDefault > 0, "exact dispatch names a missing variant");
+static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRows > 0 && kHopLongRows > 0 &&
+                  kHopWide > 0 && kHopFewRows > 0,
+              "exact dispatch names a missing variant");
 
 // From the round-2 MI355X sweeps (tools/sweep_exact.py -> profiles/r02/sweep_exact*.jsonl; the
-// last, sweep_exact7_x_lds.jsonl, over 11 shapes from 4200^2 to 65536^2 and 4194304 x 512). The
-// forms with x in the LDS ring and the LDS reads pipelined one chunk group ahead
-// (gemv_seq_x) beat the scalar-x forms wherever the chain, not HBM, was the limit (4096 x 16384:
-// 430 -> 185 us; 16384^2: 329 -> 323 us) and tie them at full occupancy. >= 65536 rows: 64-row
-// waves, 512-B row segments for short rows (K <= 1024: 4194304 x 512) and 256-B ones otherwise;
-// fewer rows: 32-row waves with 1-KiB segments, within 1.1x of the best form on every swept
-// shape below 65536 rows.
+// dispatch below from sweep_exact9_hop.jsonl, 23 shapes from 600^2 to 131072^2 and
+// 4194304 x 512). Tall shapes keep the LDS forms — >= 16384 rows, 64-row waves (512-B row
+// segments for short rows, K <= 1024; 256-B ones otherwise), 12288 .. 16383 rows 32-row waves
+// with 1-KiB segments — except for very long rows (K >= 65536: 65536^2 and 131072^2, 2-6 %
+// faster with 8 lanes per row and 24 segments in flight). Below that the chain-hopping register forms win — up to 3.2x on the
+// reference's R x 60000 shapes — by how many lanes share a row: 8 lanes x 16 B per row where
+// >= 6144 rows (or K <= 8192) give enough waves, 16 lanes x 32 B for 2048 .. 6143 rows,
+// 32 lanes x 64 B for fewer rows with K > 4096 (the chain dominates: longer runs per lane
+// between hops), 16 x 32 B for short ones.
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     if (!seq_vec_ok(lda, aligned)) return kSeqScalar;
-    if (M >= 65536) return K <= 1024 ? kSeqShortRows : kSeqManyRows;
-    return kSeqDefault;
+    if (M >= 16384) return K <= 1024 ? kSeqShortRows : K >= 65536 ? kHopLongRows : kSeqManyRows;
+    if (M >= 12288) return kSeqMidRows;
+    if (M >= 6144) return kHopRows;
+    if (M >= 2048) return K <= 8192 ? kHopRows : kHopWide;
+    return K <= 4096 ? kHopWide : kHopFewRows;
 }
 
 }  // namespace mvg
@@ -404,7 +528,7 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
     const int v = variant == 0 ? pick_seq_variant(lda, m, k, aligned) : variant;
     if (kSeqVariants[v].vec && !seq_vec_ok(lda, aligned))
-        return fail(MVG_E_INVALID, "mvg_gemv_exact: LDS-DMA variant needs 16-B aligned A, x and an even lda < 2^23");
+        return fail(MVG_E_INVALID, "mvg_gemv_exact: 16-B variant needs 16-B aligned A, x and an even lda < 2^23");
     // k == 0 runs the kernel too: every row's sum stays 0 (the reference's `sum = 0`)
     // grid-size cap: fewer than 2^32 threads per launch
     const int64_t max_rows = ((1ll << 26) - 1) * kSeqVariants[v].rows;

@@ -67,7 +67,7 @@ def test_gemv_exact_padded_lda_misaligned_and_k_zero():
     mm.gemv(dA.ptr + 8, lda, dx.ptr + 8, dy.ptr, m, k, None, 0, exact=True)
     _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
     assert np.array_equal(dy.download(), want)
-    with pytest.raises(_lib.MvgError):  # an LDS-DMA variant refuses the misaligned operands
+    with pytest.raises(_lib.MvgError):  # a 16-B variant refuses the misaligned operands
         mm.gemv(dA.ptr + 8, lda, dx.ptr + 8, dy.ptr, m, k, None, 2, exact=True)
     dy.upload(np.full(m, 7.0))
     mm.gemv(dA.ptr, lda, dx.ptr, dy.ptr, m, 0, None, 0, exact=True)
