@@ -32,6 +32,11 @@ namespace {
 inline bool is_space(char c) {
     return c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
 }
+// the same test as 0/1 arithmetic ('\t' ... '\r' are 9 ... 13)
+inline unsigned is_space_bits(char c) {
+    const unsigned u = (unsigned char)c;
+    return (unsigned)(u == 32u) | (unsigned)(u - 9u < 5u);
+}
 
 constexpr double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
@@ -98,6 +103,117 @@ inline bool parse_fast(const char* p, const char* end, double* out) {
     return true;
 }
 
+// The reference's own token shape, [-]digits[.digits] with at most 15 digits in all (its inputs
+// are "%.4f"): m < 10^15 < 2^53 and 10^f (f <= 15 fraction digits) are exact doubles, so
+// m / 10^f is strtod's correctly rounded result — the same double parse_fast gives, which strips
+// zeros first (the rational m / 10^f is the same either way). Leading zeros count as digits
+// here, which only makes the check stricter. The fraction is read 8 bytes at a time (SWAR):
+// the bytes that are digits are found with one add and mask, and up to 8 of them are converted
+// with three multiplies. p points at the token's first byte; returns the byte after the token,
+// or nullptr (nothing written) for any other shape, or when fewer than 8 bytes follow the
+// point (the caller's general path handles the file's last bytes).
+inline const char* parse_plain(const char* p, const char* end, double* out) {
+    const bool neg = *p == '-';
+    p += neg;
+    uint64_t m = 0;
+    int nd = 0;
+    for (; p < end; ++p) {
+        const unsigned d = (unsigned)(unsigned char)*p - '0';
+        if (d >= 10) break;
+        m = m * 10 + d;
+        ++nd;
+    }
+    int nf = 0;
+    if (p < end && *p == '.') {
+        ++p;
+        if (end - p < 8) return nullptr;
+        uint64_t w;
+        memcpy(&w, p, 8);
+        const uint64_t a = w ^ 0x3030303030303030ull;  // digit bytes -> 0 ... 9
+        const uint64_t nondigit = ((((a & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | a) &
+                                   0x8080808080808080ull);
+        if (nondigit == 0) return nullptr;  // 8 or more fraction digits: the general path
+        nf = __builtin_ctzll(nondigit) >> 3;
+        if (nf > 0) {
+            uint64_t v = a << (8 * (8 - nf));  // digits into the top bytes, zeros before them
+            v = ((v & 0x0F0F0F0F0F0F0F0Full) * 2561) >> 8;
+            v = ((v & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
+            v = ((v & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+            m = m * (uint64_t)kPow10[nf] + v;
+            nd += nf;
+        }
+        p += nf;
+    }
+    if (nd == 0 || nd > 15 || (p < end && !is_space(*p))) return nullptr;
+    const double v = nf > 0 ? (double)(int64_t)m / kPow10[nf] : (double)(int64_t)m;  // m < 10^15
+    *out = neg ? -v : v;
+    return p;
+}
+
+// The two per-thread loops are built for AVX-512BW and AVX2 beside the baseline x86-64 and
+// picked at load time (the library is built here and runs on the GPU box's host).
+#define MVG_CPU_CLONES __attribute__((target_clones("avx512bw", "avx2", "default")))
+
+// Tokens in [p, end): a token starts where a non-space follows a space (or at p: every range
+// but the first starts on whitespace). Branch-free over bytes, so the loop vectorises.
+MVG_CPU_CLONES int64_t count_tokens(const char* p, const char* end) {
+    if (p >= end) return 0;
+    const unsigned char* b = (const unsigned char*)p;
+    const size_t len = (size_t)(end - p);
+    uint64_t k = !is_space(p[0]);
+    for (size_t i = 1; i < len; ++i) k += is_space_bits((char)b[i - 1]) & ~is_space_bits((char)b[i]) & 1u;
+    return (int64_t)k;
+}
+
+// One token of [p, end) into *out (p at the token's first byte); returns the byte after it.
+// Sets *bad if the token is not a number.
+inline const char* parse_token(const char* p, const char* end, double* out, int* bad) {
+    if (const char* q = parse_plain(p, end, out)) return q;
+    const char* j = p;
+    while (j < end && !is_space(*j)) ++j;
+    const size_t tl = (size_t)(j - p);
+    char buf[128];
+    if (parse_fast(p, j, out)) {
+        // exact: the value strtod would return
+    } else if (tl < sizeof(buf)) {
+        memcpy(buf, p, tl);
+        buf[tl] = '\0';
+        char* ep = nullptr;
+        *out = strtod(buf, &ep);
+        *bad |= ep == buf;
+    } else {
+        std::string tok(p, tl);
+        char* ep = nullptr;
+        *out = strtod(tok.c_str(), &ep);
+        *bad |= ep == tok.c_str();
+    }
+    return j;
+}
+
+// kStreams consecutive ranges [p[s], end[s]) into out[k0[s] ...], stopping at out[n - 1], one
+// token of each in turn: a token's end (hence the next one's address) depends on the bytes just
+// parsed, so one range alone is a chain of dependent loads; four interleaved chains keep the
+// core busy. Returns 1 if a token is not a number, else 0.
+constexpr int kStreams = 4;
+MVG_CPU_CLONES int parse_ranges(const char* const* p0, const char* const* end, const int64_t* k0, int64_t n,
+                                double* out) {
+    const char* p[kStreams];
+    int64_t k[kStreams];
+    for (int s = 0; s < kStreams; ++s) p[s] = p0[s], k[s] = k0[s];
+    int bad = 0;
+    for (;;) {
+        bool any = false;
+        for (int s = 0; s < kStreams; ++s) {
+            while (p[s] < end[s] && is_space(*p[s])) ++p[s];
+            if (p[s] >= end[s] || k[s] >= n) continue;
+            any = true;
+            p[s] = parse_token(p[s], end[s], &out[k[s]], &bad);
+            ++k[s];
+        }
+        if (!any) return bad;
+    }
+}
+
 // Parse the first n tokens of the file into out. Returns MVG_OK / MVG_E_IO.
 int parse_file(const std::string& path, int64_t n, double* out) {
     int fd = open(path.c_str(), O_RDONLY);
@@ -119,46 +235,46 @@ int parse_file(const std::string& path, int64_t n, double* out) {
     const char* base = (const char*)mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
     close(fd);
     if (base == MAP_FAILED) return fail(MVG_E_IO, "mmap failed for '" + path + "'");
-    (void)madvise((void*)base, len, MADV_SEQUENTIAL);
 
     int nt = (int)std::thread::hardware_concurrency();
     if (const char* e = getenv("MVG_THREADS")) nt = atoi(e);
     if (nt < 1) nt = 1;
     if (nt > 64) nt = 64;
     if (len < (1u << 20)) nt = 1;
-    // range t = [cut[t], cut[t+1]); cuts moved forward to the next whitespace so that no
-    // token straddles two ranges.
-    std::vector<size_t> cut(nt + 1);
-    for (int t = 0; t <= nt; ++t) {
-        size_t c = len * (size_t)t / (size_t)nt;
-        if (t > 0 && t < nt)
+    // nr = nt * kStreams ranges, range r = [cut[r], cut[r+1]), thread t taking ranges
+    // [t*kStreams, +kStreams); cuts moved forward to the next whitespace so that no token
+    // straddles two ranges.
+    const int nr = nt * kStreams;
+    std::vector<size_t> cut(nr + 1);
+    for (int r = 0; r <= nr; ++r) {
+        size_t c = len * (size_t)r / (size_t)nr;
+        if (r > 0 && r < nr)
             while (c < len && !is_space(base[c])) ++c;
-        cut[t] = c;
+        cut[r] = c;
     }
-    for (int t = 1; t <= nt; ++t)
-        if (cut[t] < cut[t - 1]) cut[t] = cut[t - 1];
+    for (int r = 1; r <= nr; ++r)
+        if (cut[r] < cut[r - 1]) cut[r] = cut[r - 1];
 
-    std::vector<int64_t> count(nt, 0);
+    std::vector<int64_t> count(nr, 0);
     {
         std::vector<std::thread> th;
         for (int t = 0; t < nt; ++t)
             th.emplace_back([&, t] {
-                int64_t k = 0;
-                bool in = false;
-                for (size_t i = cut[t]; i < cut[t + 1]; ++i) {
-                    const bool sp = is_space(base[i]);
-                    if (!sp && !in) ++k;
-                    in = !sp;
-                }
-                count[t] = k;
+#ifdef MADV_POPULATE_READ
+                // map this thread's pages in one call (page-table batches, no fault per page)
+                const size_t lo = cut[t * kStreams] & ~(size_t)4095, hi = cut[(t + 1) * kStreams];
+                if (hi > lo) (void)madvise((void*)(base + lo), hi - lo, MADV_POPULATE_READ);
+#endif
+                for (int r = t * kStreams; r < (t + 1) * kStreams; ++r)
+                    count[r] = count_tokens(base + cut[r], base + cut[r + 1]);
             });
         for (auto& x : th) x.join();
     }
-    std::vector<int64_t> start(nt + 1, 0);
-    for (int t = 0; t < nt; ++t) start[t + 1] = start[t] + count[t];
-    if (start[nt] < n) {
+    std::vector<int64_t> start(nr + 1, 0);
+    for (int r = 0; r < nr; ++r) start[r + 1] = start[r] + count[r];
+    if (start[nr] < n) {
         munmap((void*)base, len);
-        return fail(MVG_E_IO, "'" + path + "' holds " + std::to_string(start[nt]) +
+        return fail(MVG_E_IO, "'" + path + "' holds " + std::to_string(start[nr]) +
                                   " values, expected " + std::to_string(n));
     }
     std::vector<int> bad(nt, 0);
@@ -166,33 +282,11 @@ int parse_file(const std::string& path, int64_t n, double* out) {
         std::vector<std::thread> th;
         for (int t = 0; t < nt; ++t)
             th.emplace_back([&, t] {
-                int64_t k = start[t];
-                size_t i = cut[t];
-                const size_t end = cut[t + 1];
-                char buf[128];
-                while (i < end && k < n) {
-                    while (i < end && is_space(base[i])) ++i;
-                    if (i >= end) break;
-                    size_t j = i;
-                    while (j < end && !is_space(base[j])) ++j;
-                    const size_t tl = j - i;
-                    if (parse_fast(base + i, base + j, &out[k])) {
-                        // exact: the value strtod would return
-                    } else if (tl < sizeof(buf)) {
-                        memcpy(buf, base + i, tl);
-                        buf[tl] = '\0';
-                        char* ep = nullptr;
-                        out[k] = strtod(buf, &ep);
-                        if (ep == buf) bad[t] = 1;
-                    } else {
-                        std::string tok(base + i, tl);
-                        char* ep = nullptr;
-                        out[k] = strtod(tok.c_str(), &ep);
-                        if (ep == tok.c_str()) bad[t] = 1;
-                    }
-                    ++k;
-                    i = j;
-                }
+                const char* p[kStreams];
+                const char* e[kStreams];
+                for (int s = 0; s < kStreams; ++s)
+                    p[s] = base + cut[t * kStreams + s], e[s] = base + cut[t * kStreams + s + 1];
+                bad[t] = parse_ranges(p, e, &start[t * kStreams], n, out);
             });
         for (auto& x : th) x.join();
     }

@@ -248,6 +248,32 @@ def test_parser_is_bit_identical_to_strtod(tmp_path):
     assert not bad, bad[:10]
 
 
+def test_parser_plain_tokens_many_ranges(tmp_path):
+    # the 8-bytes-at-a-time path for [-]digits[.digits] tokens: every fraction length 0 ... 9
+    # (8 and more leave it for the general path), 1 ... 16 digits in all (15 is its limit),
+    # mixed separators, over a multi-MiB file so that every thread's four interleaved ranges and
+    # their cut points are exercised; the last token ends the file without a newline, fewer
+    # than 8 bytes after its point
+    rng = np.random.default_rng(11)
+    toks = []
+    for i in range(400_000):
+        ni, nf = int(rng.integers(0, 10)), int(rng.integers(0, 10))
+        ip = "".join(str(d) for d in rng.integers(0, 10, ni))
+        fp = "".join(str(d) for d in rng.integers(0, 10, nf))
+        t = (ip or ("0" if nf == 0 else "")) + ("." + fp if nf or i % 7 == 0 else "")
+        toks.append(("-" if i % 3 == 0 else "") + t)
+    toks += ["123456789012345", "12345678901234.5", "1234567890123456", "0.000000000000001", "-0.0000",
+             "7.", ".5", "-.5"]
+    seps = [" ", "\n", "\t", "\r\n", "  "]
+    text = "".join(t + seps[i % len(seps)] for i, t in enumerate(toks)) + "3.25"
+    toks.append("3.25")
+    (tmp_path / f"vector_{len(toks)}.txt").write_text(text)
+    got = mm.load_vec(len(toks), str(tmp_path))
+    want = np.array([float(t) for t in toks])
+    bad = [t for t, g, w in zip(toks, got.view(np.uint64), want.view(np.uint64)) if g != w]
+    assert not bad, bad[:10]
+
+
 def test_write_vec_roundtrips(tmp_path):
     v = np.array([222.19999999999999, 1e-300, -0.0, 3.141592653589793, 1076.4842229100022])
     mm.write_vec(str(tmp_path / "vector_5.txt"), v)
