@@ -175,13 +175,16 @@ const char* mvg_gemv_multi_variant_name(int variant);
  *   sum = 0; for j < k: sum = round(sum + round(A[i*lda + j] * x[j]))
  * (src/matr_utils.c:87-93: a rounded multiply then a rounded add, left to right, no FMA), so
  * y is bit-identical to multiply_std_rowwise on the same inputs (and to the strip sums of
- * multiply_colwise, src/multiplier_colwise.c:107-122). One lane per row; rows stream through
- * LDS (csrc/gemv_exact.hip). Any lda >= k and alignment (16-B aligned A, x with an even lda and
- * 64*lda*8 < 2^32 take the LDS-DMA path, anything else a per-lane 8-B path). */
+ * multiply_colwise, src/multiplier_colwise.c:107-122). Tall shapes: one lane per row, rows
+ * streamed through LDS; fewer rows (< 12288) or K >= 65536: several lanes per row, the running
+ * sum handed lane to lane in column order (csrc/gemv_exact.hip). Any lda >= k and alignment
+ * (16-B aligned A, x with an even lda and 64*lda*8 < 2^32 take the 16-B paths, anything else a
+ * per-lane 8-B path). */
 int mvg_gemv_exact(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                    int64_t m, int64_t k, void* stream);
-/* explicit exact variant (0 = auto; names via mvg_gemv_exact_variant_name: seq_t<T>_b<NB>
- * LDS-DMA tiles of 2T columns with NB buffers, seq_scalar the 8-B path) */
+/* explicit exact variant (0 = auto; names via mvg_gemv_exact_variant_name: seq_r<RW>_t<T>_b<NB>
+ * and seqx_* RW-row LDS-DMA tiles of 2T columns with NB buffers, hop_l<L>_w<W>_u<U> L lanes per
+ * row holding W columns each with U segments in flight, seq_scalar the 8-B path) */
 int mvg_gemv_exact_variant(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                            int64_t m, int64_t k, int variant, void* stream);
 int mvg_gemv_exact_variant_count(void);
