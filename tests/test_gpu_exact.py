@@ -44,12 +44,32 @@ def test_gemv_exact_every_variant_is_the_reference_sum(m, k):
     x = signed(oracle.synth(1, k, 4242)[0], k)
     want = oracle.multiply_std_rowwise(A, x)
     for v, name in exact_variants():
-        if name not in ("auto", "seq_scalar") and k % 2:  # the LDS-DMA forms need an even lda
+        if name not in ("auto", "seq_scalar") and k % 2:  # the 16-B forms need an even lda
             with pytest.raises(_lib.MvgError):
                 mm.multiply_std_rowwise(A, x, variant=v, exact=True)
             continue
         y = mm.multiply_std_rowwise(A, x, variant=v, exact=True)
         assert np.array_equal(y, want), (name, m, k, max_rel(y, want))
+
+
+def test_gemv_exact_hop_segment_edges():
+    # the chain-hopping forms (hop_l<L>_w<W>_u<U>): a segment is S = L*W columns and U segments
+    # are in flight; after an odd number of segments the chain ends in lane L-1, after an even
+    # number in lane 0, so every variant is run with odd and even segment counts, with and
+    # without leftover segments (nseg % U), a column tail, no whole segment at all, and a
+    # last wave with rows to spare
+    for v, name in exact_variants():
+        if not name.startswith("hop_"):
+            continue
+        L, W, U = (int(part[1:]) for part in name.split("_")[1:4])
+        S = L * W
+        m = 3 * (64 // L) + 1
+        for k in (S - 2, S, 3 * S + 2, (U + 1) * S, (U + 1) * S + 2, (U + 2) * S, 2 * U * S, 2 * U * S + 2,
+                  (3 * U - 1) * S):
+            A = signed(oracle.synth(m, k, 42), k)
+            x = signed(oracle.synth(1, k, 4242)[0], k + 1)
+            y = mm.multiply_std_rowwise(A, x, variant=v, exact=True)
+            assert np.array_equal(y, oracle.multiply_std_rowwise(A, x)), (name, m, k)
 
 
 def test_gemv_exact_padded_lda_misaligned_and_k_zero():
