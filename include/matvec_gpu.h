@@ -14,6 +14,7 @@
  *                               (also the strip GEMV that multiply_colwise computes as
  *                                scale-then-row-sum,          src/multiplier_colwise.c:105-122)
  *   mvg_gemv_exact           <- the same, bit for bit (the reference's sequential sum)
+ *   mvg_multiply_std_rowwise <- multiply_std_rowwise itself on host pointers (matr_utils.h:4-10)
  *   mvg_grid_shape           <- get_2_most_closest_multipliers src/utils.c:26-37
  *   mvg_plan_shard           <- local_n / local_n_rows / local_n_cols arithmetic
  *                               src/multiplier_rowwise.c:93, src/multiplier_colwise.c:349,
@@ -182,6 +183,15 @@ const char* mvg_gemv_multi_variant_name(int variant);
  * per-lane 8-B path). */
 int mvg_gemv_exact(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                    int64_t m, int64_t k, void* stream);
+/* The reference's in-process call on host pointers, src/matr_utils.h:4-10:
+ *   void multiply_std_rowwise(double* matrix, double* vector, long n_rows, long n_cols, double* result);
+ * row-major matrix (n_rows x n_cols), vector (n_cols), result (n_rows), all caller-owned host
+ * memory, on the calling thread's current device: copies A and x over, runs mvg_gemv_exact
+ * (exact != 0: result bit-identical to the reference's) or mvg_gemv (exact == 0: within 1e-12),
+ * copies y back and waits. Device buffers are kept per thread and grown as needed; all-zero /
+ * null arguments release them. */
+int mvg_multiply_std_rowwise(const double* matrix, const double* vector, int64_t n_rows, int64_t n_cols,
+                             double* result, int exact);
 /* explicit exact variant (0 = auto; names via mvg_gemv_exact_variant_name: seq_r<RW>_t<T>_b<NB>
  * and seqx_* RW-row LDS-DMA tiles of 2T columns with NB buffers, hop_l<L>_w<W>_u<U> L lanes per
  * row holding W columns each with U segments in flight, seq_scalar the 8-B path) */

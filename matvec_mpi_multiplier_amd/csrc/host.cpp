@@ -278,6 +278,63 @@ int mvg_stream_sync(void* stream) {
     MVG_HIP(hipStreamSynchronize((hipStream_t)stream));
     return MVG_OK;
 }
+// ------------------------------------------------------------------ the reference's in-process call
+// multiply_std_rowwise(matrix, vector, n_rows, n_cols, result) (src/matr_utils.h:4-10,
+// src/matr_utils.c:86-96) on host pointers, on the calling thread's current device: A and x go
+// over, the GEMV runs (exact != 0: the reference's own sequential sums, bit for bit; 0: the
+// tree-summed kernel, within 1e-12), y comes back. The device buffers stay with the thread and
+// grow as needed, so a loop of calls allocates once; they are released by a call with
+// n_rows = n_cols = 0 and null pointers, or at process exit.
+int mvg_multiply_std_rowwise(const double* matrix, const double* vector, int64_t n_rows, int64_t n_cols,
+                             double* result, int exact) {
+    struct Workspace {
+        int dev = -1;
+        double* buf = nullptr;
+        size_t cap = 0;  // doubles
+    };
+    thread_local Workspace ws;
+    if (n_rows < 0 || n_cols < 0) return fail(MVG_E_INVALID, "mvg_multiply_std_rowwise: negative size");
+    if (n_rows == 0 && n_cols == 0 && !matrix && !vector && !result) {
+        if (ws.buf) {
+            int cur = 0;
+            MVG_HIP(hipGetDevice(&cur));
+            MVG_HIP(hipSetDevice(ws.dev));
+            const hipError_t e = hipFree(ws.buf);
+            MVG_HIP(hipSetDevice(cur));
+            ws = Workspace{};
+            MVG_HIP(e);
+        }
+        return MVG_OK;
+    }
+    if (n_rows == 0) return MVG_OK;
+    if (!result || (n_cols > 0 && (!matrix || !vector)))
+        return fail(MVG_E_INVALID, "mvg_multiply_std_rowwise: null pointer");
+    int dev = 0;
+    MVG_HIP(hipGetDevice(&dev));
+    auto even = [](int64_t n) { return (size_t)((n + 1) & ~(int64_t)1); };  // 16-B aligned parts
+    const size_t na = even(n_rows * n_cols), nx = even(n_cols), need = na + nx + even(n_rows);
+    if (ws.dev != dev || ws.cap < need) {
+        if (ws.buf) {
+            MVG_HIP(hipSetDevice(ws.dev));
+            (void)hipFree(ws.buf);
+            MVG_HIP(hipSetDevice(dev));
+            ws = Workspace{};
+        }
+        void* p = nullptr;
+        if (const int rc = mvg_malloc(&p, need * sizeof(double)); rc != MVG_OK) return rc;
+        ws.dev = dev, ws.buf = (double*)p, ws.cap = need;
+    }
+    double *dA = ws.buf, *dx = dA + na, *dy = dx + nx;
+    MVG_HIP(hipMemcpyAsync(dA, matrix, (size_t)(n_rows * n_cols) * sizeof(double), hipMemcpyHostToDevice, nullptr));
+    MVG_HIP(hipMemcpyAsync(dx, vector, (size_t)n_cols * sizeof(double), hipMemcpyHostToDevice, nullptr));
+    const int rc = exact ? mvg_gemv_exact(dA, n_cols, dx, dy, n_rows, n_cols, nullptr)
+                         : mvg_gemv(dA, n_cols, dx, dy, n_rows, n_cols, nullptr);
+    if (rc != MVG_OK) return rc;
+    MVG_HIP(hipMemcpyAsync(result, dy, (size_t)n_rows * sizeof(double), hipMemcpyDeviceToHost, nullptr));
+    MVG_HIP(hipStreamSynchronize(nullptr));
+    return MVG_OK;
+}
+
 int mvg_host_register(void* ptr, size_t bytes) {
     MVG_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
     return MVG_OK;

@@ -205,3 +205,35 @@ def test_engine_exact_shard_products_and_combines_at_p_gt_1(golden, manifest):
             assert max_rel(y, golden[key]) <= 1e-12, key
         else:
             assert np.array_equal(y, golden[key]), key
+
+
+def test_multiply_std_rowwise_host_entry_point():
+    # mvg_multiply_std_rowwise: the reference's in-process call (matr_utils.h:4-10) on host
+    # pointers — bit for bit with exact=1, within the bar otherwise; the per-thread device
+    # buffers grow across calls of rising size and are released by the all-null call
+    import ctypes as C
+
+    lib = _lib.lib
+
+    def call(A, x, exact):
+        y = np.full(A.shape[0], np.nan)
+        ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        _lib.check(lib.mvg_multiply_std_rowwise(ptr(A), ptr(x), A.shape[0], A.shape[1], ptr(y), exact), "call")
+        return y
+
+    from conftest import GOLDEN_DIR
+
+    A = np.ascontiguousarray(np.loadtxt(os.path.join(GOLDEN_DIR, "matrix_4_8.txt")).reshape(4, 8))
+    x = np.ascontiguousarray(np.loadtxt(os.path.join(GOLDEN_DIR, "vector_8.txt")).reshape(8))
+    assert ["%.17g" % v for v in call(A, x, 1)] == ["222.19999999999999", "196.55000000000001",
+                                                  "191.56999999999999", "232.90000000000001"]
+    for m, k in [(3, 5), (7, 20001), (130, 16388), (4200, 4200), (1200, 6000)]:
+        A = np.ascontiguousarray(signed(oracle.synth(m, k, 42), k))
+        x = np.ascontiguousarray(signed(oracle.synth(1, k, 4242)[0], m))
+        want = oracle.multiply_std_rowwise(A, x)
+        assert np.array_equal(call(A, x, 1), want), (m, k)
+        assert max_rel(call(A, x, 0), want) <= 1e-12, (m, k)
+    assert np.array_equal(call(np.zeros((5, 0)), np.zeros(0), 1), np.zeros(5))  # sum = 0
+    _lib.check(lib.mvg_multiply_std_rowwise(None, None, 0, 0, None, 0), "release")
+    with pytest.raises(_lib.MvgError):
+        _lib.check(lib.mvg_multiply_std_rowwise(None, None, 3, 3, None, 1), "null")
