@@ -228,11 +228,13 @@ def test_multiply_std_rowwise_host_entry_point():
     assert ["%.17g" % v for v in call(A, x, 1)] == ["222.19999999999999", "196.55000000000001",
                                                   "191.56999999999999", "232.90000000000001"]
     for m, k in [(3, 5), (7, 20001), (130, 16388), (4200, 4200), (1200, 6000)]:
-        A = np.ascontiguousarray(signed(oracle.synth(m, k, 42), k))
-        x = np.ascontiguousarray(signed(oracle.synth(1, k, 4242)[0], m))
+        # the reference's own inputs (non-negative: the 1e-12 relative bar applies row by row)
+        A, x = oracle.synth(m, k, 42), oracle.synth(1, k, 4242)[0]
         want = oracle.multiply_std_rowwise(A, x)
-        assert np.array_equal(call(A, x, 1), want), (m, k)
         assert max_rel(call(A, x, 0), want) <= 1e-12, (m, k)
+        # mixed signs: bit for bit still
+        A, x = np.ascontiguousarray(signed(A, k)), np.ascontiguousarray(signed(x, m))
+        assert np.array_equal(call(A, x, 1), oracle.multiply_std_rowwise(A, x)), (m, k)
     assert np.array_equal(call(np.zeros((5, 0)), np.zeros(0), 1), np.zeros(5))  # sum = 0
     _lib.check(lib.mvg_multiply_std_rowwise(None, None, 0, 0, None, 0), "release")
     with pytest.raises(_lib.MvgError):
