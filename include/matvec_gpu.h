@@ -179,8 +179,8 @@ const char* mvg_gemv_multi_variant_name(int variant);
  * multiply_colwise, src/multiplier_colwise.c:107-122). Tall shapes: one lane per row, rows
  * streamed through LDS; fewer rows (< 12288) or K >= 65536: several lanes per row, the running
  * sum handed lane to lane in column order (csrc/gemv_exact.hip). Any lda >= k and alignment
- * (16-B aligned A, x with an even lda and 64*lda*8 < 2^32 take the 16-B paths, anything else a
- * per-lane 8-B path). */
+ * (16-B aligned A, x with an even lda take the 16-B paths — the LDS ones only for lda < 2^23 —
+ * anything else a per-lane 8-B path). */
 int mvg_gemv_exact(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                    int64_t m, int64_t k, void* stream);
 /* The reference's in-process call on host pointers, src/matr_utils.h:4-10:

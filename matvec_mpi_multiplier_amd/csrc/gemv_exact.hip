@@ -416,15 +416,18 @@ typedef void (*seq_fn)(const double*, int64_t, const double*, double*, int64_t, 
 struct SeqVariant {
     const char* name;
     seq_fn fn;
-    bool vec;  // 16-B loads (LDS-DMA or plain): needs 16-B aligned A, x and an even lda
+    int needs;  // operand requirements: kAnyOperands, kVec16 or kVec16Lda23 (below)
     int rows;  // rows per one-wave workgroup
 };
 
-#define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, true, RW}
-#define HOP(L, W, U) {"hop_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U>, true, 64 / L}
+// kVec16: 16-B loads, so 16-B aligned A and x and an even lda; kVec16Lda23: also 32-bit
+// per-lane LDS-DMA offsets over 64 rows of lda (lda < 2^23)
+constexpr int kAnyOperands = 0, kVec16 = 1, kVec16Lda23 = 2;
+#define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, kVec16Lda23, RW}
+#define HOP(L, W, U) {"hop_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U>, kVec16, 64 / L}
 static constexpr SeqVariant kSeqVariants[] = {
-    {"auto", nullptr, false, 64},          // 0
-    {"seq_scalar", gemv_seq_scalar, false, 64},
+    {"auto", nullptr, kAnyOperands, 64},  // 0
+    {"seq_scalar", gemv_seq_scalar, kAnyOperands, 64},
     // x through the scalar cache (the first form; kept for comparison)
     SEQ(64, 16, 2),   // LDS per wave: NB x RW x 16T bytes; 32 KiB
     SEQ(64, 32, 2),   // 64 KiB
@@ -432,12 +435,12 @@ static constexpr SeqVariant kSeqVariants[] = {
     SEQ(32, 64, 2),   // 64 KiB
     SEQ(16, 64, 2),   // 32 KiB
     // x through the LDS ring, LDS reads one chunk group ahead of the sums
-    {"seqx_r32_t64_b2_g8", gemv_seq_x<32, 64, 2, 8>, true, 32},
-    {"seqx_r32_t64_b2_g16", gemv_seq_x<32, 64, 2, 16>, true, 32},
-    {"seqx_r64_t16_b2_g8", gemv_seq_x<64, 16, 2, 8>, true, 64},
-    {"seqx_r64_t32_b2_g8", gemv_seq_x<64, 32, 2, 8>, true, 64},
-    {"seqx_r16_t64_b2_g8", gemv_seq_x<16, 64, 2, 8>, true, 16},
-    {"seqx_r16_t32_b4_g8", gemv_seq_x<16, 32, 4, 8>, true, 16},
+    {"seqx_r32_t64_b2_g8", gemv_seq_x<32, 64, 2, 8>, kVec16Lda23, 32},
+    {"seqx_r32_t64_b2_g16", gemv_seq_x<32, 64, 2, 16>, kVec16Lda23, 32},
+    {"seqx_r64_t16_b2_g8", gemv_seq_x<64, 16, 2, 8>, kVec16Lda23, 64},
+    {"seqx_r64_t32_b2_g8", gemv_seq_x<64, 32, 2, 8>, kVec16Lda23, 64},
+    {"seqx_r16_t64_b2_g8", gemv_seq_x<16, 64, 2, 8>, kVec16Lda23, 16},
+    {"seqx_r16_t32_b4_g8", gemv_seq_x<16, 32, 4, 8>, kVec16Lda23, 16},
     // L lanes per row, the chain hopping across them (registers, no LDS)
     HOP(64, 8, 4),
     HOP(32, 8, 4),
@@ -454,8 +457,11 @@ static constexpr SeqVariant kSeqVariants[] = {
 };
 constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
 
-// the LDS-DMA path's per-lane offsets span 64 rows of lda in 32 bits
-static bool seq_vec_ok(int64_t lda, bool aligned) { return aligned && lda % 2 == 0 && lda < (1ll << 23); }
+static bool operands_ok(int needs, int64_t lda, bool aligned) {
+    if (needs == kAnyOperands) return true;
+    if (!aligned || lda % 2 != 0) return false;
+    return needs == kVec16 || lda < (1ll << 23);
+}
 
 template <size_t N>
 constexpr int seq_id(const SeqVariant (&table)[N], const char* name) {
@@ -474,7 +480,10 @@ constexpr int kHopRows = seq_id(kSeqVariants, "hop_l8_w2_u16");
 constexpr int kHopLongRows = seq_id(kSeqVariants, "hop_l8_w2_u24");
 constexpr int kHopWide = seq_id(kSeqVariants, "hop_l16_w4_u8");
 constexpr int kHopFewRows = seq_id(kSeqVariants, "hop_l32_w8_u4");
-static_assert(kSeqScalar > 0 && !kSeqVariants[kSeqScalar].vec, "8-B exact fallback");
+static_assert(kSeqScalar > 0 && kSeqVariants[kSeqScalar].needs == kAnyOperands, "8-B exact fallback");
+static_assert(kSeqVariants[kHopRows].needs == kVec16 && kSeqVariants[kHopLongRows].needs == kVec16 &&
+                  kSeqVariants[kHopFewRows].needs == kVec16,
+              "the dispatch's choice for lda >= 2^23 must not need 32-bit LDS offsets");
 static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRows > 0 && kHopLongRows > 0 &&
                   kHopWide > 0 && kHopFewRows > 0,
               "exact dispatch names a missing variant");
@@ -490,7 +499,8 @@ static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRo
 // 32 lanes x 64 B for fewer rows with K > 4096 (the chain dominates: longer runs per lane
 // between hops), 16 x 32 B for short ones.
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
-    if (!seq_vec_ok(lda, aligned)) return kSeqScalar;
+    if (!operands_ok(kVec16, lda, aligned)) return kSeqScalar;
+    if (lda >= (1ll << 23)) return M >= 6144 ? kHopLongRows : kHopFewRows;  // rows of >= 8 M columns
     if (M >= 16384) return K <= 1024 ? kSeqShortRows : K >= 65536 ? kHopLongRows : kSeqManyRows;
     if (M >= 12288) return kSeqMidRows;
     if (M >= 6144) return kHopRows;
@@ -527,8 +537,10 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
     }
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
     const int v = variant == 0 ? pick_seq_variant(lda, m, k, aligned) : variant;
-    if (kSeqVariants[v].vec && !seq_vec_ok(lda, aligned))
-        return fail(MVG_E_INVALID, "mvg_gemv_exact: 16-B variant needs 16-B aligned A, x and an even lda < 2^23");
+    if (!operands_ok(kSeqVariants[v].needs, lda, aligned))
+        return fail(MVG_E_INVALID, kSeqVariants[v].needs == kVec16
+                                       ? "mvg_gemv_exact: 16-B variant needs 16-B aligned A, x and an even lda"
+                                       : "mvg_gemv_exact: LDS-DMA variant needs 16-B aligned A, x and an even lda < 2^23");
     // k == 0 runs the kernel too: every row's sum stays 0 (the reference's `sum = 0`)
     // grid-size cap: fewer than 2^32 threads per launch
     const int64_t max_rows = ((1ll << 26) - 1) * kSeqVariants[v].rows;

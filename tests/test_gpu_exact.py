@@ -72,6 +72,20 @@ def test_gemv_exact_hop_segment_edges():
             assert np.array_equal(y, oracle.multiply_std_rowwise(A, x)), (name, m, k)
 
 
+def test_gemv_exact_rows_beyond_lds_offsets():
+    # lda >= 2^23 doubles: past the LDS forms' 32-bit per-lane offsets; the dispatch takes a
+    # chain-hopping form (64-bit addressing), which must still be the reference's sum
+    m, k = 3, (1 << 23) + 34
+    A = signed(oracle.synth(m, k, 42), 5)
+    x = signed(oracle.synth(1, k, 4242)[0], 6)
+    names = dict(exact_variants())
+    assert names[_lib.lib.mvg_gemv_exact_auto_variant(k, m, k)].startswith("hop_")
+    assert np.array_equal(mm.multiply_std_rowwise(A, x, exact=True), oracle.multiply_std_rowwise(A, x))
+    lds = next(v for v, name in exact_variants() if name.startswith("seqx_"))
+    with pytest.raises(_lib.MvgError):
+        mm.multiply_std_rowwise(A, x, variant=lds, exact=True)
+
+
 def test_gemv_exact_padded_lda_misaligned_and_k_zero():
     m, k, lda = 130, 300, 512
     full = oracle.synth(m, lda, 42)
