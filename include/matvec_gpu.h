@@ -180,7 +180,7 @@ const char* mvg_gemv_multi_variant_name(int variant);
  * streamed through LDS; fewer rows (< 12288) or K >= 65536: several lanes per row, the running
  * sum handed lane to lane in column order (csrc/gemv_exact.hip). Any lda >= k and alignment
  * (16-B aligned A, x with an even lda take the 16-B paths — the LDS ones only for lda < 2^23 —
- * anything else a per-lane 8-B path). */
+ * anything else the lane-sharing forms with 8-B loads). */
 int mvg_gemv_exact(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                    int64_t m, int64_t k, void* stream);
 /* The reference's in-process call on host pointers, src/matr_utils.h:4-10:
@@ -194,7 +194,8 @@ int mvg_multiply_std_rowwise(const double* matrix, const double* vector, int64_t
                              double* result, int exact);
 /* explicit exact variant (0 = auto; names via mvg_gemv_exact_variant_name: seq_r<RW>_t<T>_b<NB>
  * and seqx_* RW-row LDS-DMA tiles of 2T columns with NB buffers, hop_l<L>_w<W>_u<U> L lanes per
- * row holding W columns each with U segments in flight, seq_scalar the 8-B path) */
+ * row holding W columns each with U segments in flight, hop8_* the same with 8-B loads (any
+ * alignment, any lda), seq_scalar a lane per row with 8-B loads) */
 int mvg_gemv_exact_variant(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                            int64_t m, int64_t k, int variant, void* stream);
 int mvg_gemv_exact_variant_count(void);

@@ -285,15 +285,32 @@ __device__ __forceinline__ double hop_segment(double sum, const dbl2x (&a)[W / 2
     return sum;
 }
 
-template <int L, int W, int U>
+// A lane's W consecutive doubles of a segment: 16-B loads, or (B8) 8-B loads, which need
+// neither a 16-B aligned A or x nor an even lda (an odd-width column strip, an offset view).
+template <int V, bool B8, bool NT>
+__device__ __forceinline__ void load_run(const double* p, dbl2x (&d)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        if constexpr (B8 && NT)
+            d[v] = dbl2x{__builtin_nontemporal_load(p + 2 * v), __builtin_nontemporal_load(p + 2 * v + 1)};
+        else if constexpr (B8)
+            d[v] = dbl2x{p[2 * v], p[2 * v + 1]};
+        else if constexpr (NT)
+            d[v] = __builtin_nontemporal_load(reinterpret_cast<const dbl2x*>(p) + v);
+        else
+            d[v] = reinterpret_cast<const dbl2x*>(p)[v];
+    }
+}
+
+template <int L, int W, int U, bool B8 = false>
 __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ x,
                                                    double* __restrict__ y, int64_t M, int64_t K) {
     static_assert(L == 1 || L == 2 || L == 4 || L == 8 || L == 16 || L == 32 || L == 64, "lanes per row");
-    static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B loads; segment pairs per unrolled step");
+    static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B pieces; segment pairs per unrolled step");
     constexpr int R = 64 / L;  // rows per wave
     constexpr int S = L * W;   // columns per segment
-    constexpr int V = W / 2;   // 16-B loads per lane per segment
+    constexpr int V = W / 2;   // 16-B pieces per lane per segment
     const int lane = threadIdx.x;
     const int c = lane % L;
     const int64_t row = (int64_t)blockIdx.x * R + lane / L;
@@ -308,10 +325,8 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             const int64_t s = i < nseg ? i : nseg - 1;
-            const dbl2x* pa = (const dbl2x*)(arow + s * S + off[i & 1]);
-            const dbl2x* px = (const dbl2x*)(x + s * S + off[i & 1]);
-#pragma unroll
-            for (int v = 0; v < V; ++v) a[i][v] = __builtin_nontemporal_load(pa + v), xv[i][v] = px[v];
+            load_run<V, B8, true>(arow + s * S + off[i & 1], a[i]);
+            load_run<V, B8, false>(x + s * S + off[i & 1], xv[i]);
             __builtin_amdgcn_sched_barrier(0);  // same load order as the loop's refills
         }
         // Whole groups of U segments, one basic block: slot i is summed, then refilled U segments
@@ -324,10 +339,8 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
                 sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
                 __builtin_amdgcn_sched_barrier(0);
                 const int64_t s = base + i + U < nseg ? base + i + U : nseg - 1;
-                const dbl2x* pa = (const dbl2x*)(arow + s * S + off[i & 1]);
-                const dbl2x* px = (const dbl2x*)(x + s * S + off[i & 1]);
-#pragma unroll
-                for (int v = 0; v < V; ++v) a[i][v] = __builtin_nontemporal_load(pa + v), xv[i][v] = px[v];
+                load_run<V, B8, true>(arow + s * S + off[i & 1], a[i]);
+                load_run<V, B8, false>(x + s * S + off[i & 1], xv[i]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -425,6 +438,7 @@ struct SeqVariant {
 constexpr int kAnyOperands = 0, kVec16 = 1, kVec16Lda23 = 2;
 #define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, kVec16Lda23, RW}
 #define HOP(L, W, U) {"hop_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U>, kVec16, 64 / L}
+#define HOP8(L, W, U) {"hop8_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U, true>, kAnyOperands, 64 / L}
 static constexpr SeqVariant kSeqVariants[] = {
     {"auto", nullptr, kAnyOperands, 64},  // 0
     {"seq_scalar", gemv_seq_scalar, kAnyOperands, 64},
@@ -454,6 +468,13 @@ static constexpr SeqVariant kSeqVariants[] = {
     HOP(8, 2, 24),
     HOP(4, 4, 8),
     HOP(4, 2, 16),
+    // the same with 8-B loads: any alignment, any lda
+    HOP8(8, 2, 16),
+    HOP8(8, 2, 24),
+    HOP8(8, 4, 8),
+    HOP8(16, 2, 16),
+    HOP8(16, 4, 8),
+    HOP8(32, 8, 4),
 };
 constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
 
@@ -480,7 +501,16 @@ constexpr int kHopRows = seq_id(kSeqVariants, "hop_l8_w2_u16");
 constexpr int kHopLongRows = seq_id(kSeqVariants, "hop_l8_w2_u24");
 constexpr int kHopWide = seq_id(kSeqVariants, "hop_l16_w4_u8");
 constexpr int kHopFewRows = seq_id(kSeqVariants, "hop_l32_w8_u4");
+// 8-B-load counterparts: any alignment, any lda
+constexpr int kHop8TallRows = seq_id(kSeqVariants, "hop8_l16_w2_u16");
+constexpr int kHop8Rows = seq_id(kSeqVariants, "hop8_l8_w2_u16");
+constexpr int kHop8Wide = seq_id(kSeqVariants, "hop8_l16_w4_u8");
+constexpr int kHop8FewRows = seq_id(kSeqVariants, "hop8_l32_w8_u4");
 static_assert(kSeqScalar > 0 && kSeqVariants[kSeqScalar].needs == kAnyOperands, "8-B exact fallback");
+static_assert(kHop8TallRows > 0 && kHop8Rows > 0 && kHop8Wide > 0 && kHop8FewRows > 0 &&
+                  kSeqVariants[kHop8TallRows].needs == kAnyOperands && kSeqVariants[kHop8Rows].needs == kAnyOperands &&
+                  kSeqVariants[kHop8Wide].needs == kAnyOperands && kSeqVariants[kHop8FewRows].needs == kAnyOperands,
+              "the dispatch's choice for any operands must take any operands");
 static_assert(kSeqVariants[kHopRows].needs == kVec16 && kSeqVariants[kHopLongRows].needs == kVec16 &&
                   kSeqVariants[kHopFewRows].needs == kVec16,
               "the dispatch's choice for lda >= 2^23 must not need 32-bit LDS offsets");
@@ -497,9 +527,16 @@ static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRo
 // reference's R x 60000 shapes — by how many lanes share a row: 8 lanes x 16 B per row where
 // >= 6144 rows (or K <= 8192) give enough waves, 16 lanes x 32 B for 2048 .. 6143 rows,
 // 32 lanes x 64 B for fewer rows with K > 4096 (the chain dominates: longer runs per lane
-// between hops), 16 x 32 B for short ones.
+// between hops), 16 x 32 B for short ones. An odd lda or operands off a 16-B boundary take the
+// same forms with 8-B loads (hop8_*; 16 lanes per row from 12288 rows: sweep_exact11_hop8.jsonl,
+// 2-36x faster than the lane-per-row 8-B kernel seq_scalar on odd widths).
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
-    if (!operands_ok(kVec16, lda, aligned)) return kSeqScalar;
+    if (!operands_ok(kVec16, lda, aligned)) {  // odd lda or operands off 16 B: the 8-B-load forms
+        if (M >= 12288) return kHop8TallRows;
+        if (M >= 6144) return kHop8Rows;
+        if (M >= 2048) return K <= 8192 ? kHop8Rows : kHop8Wide;
+        return K <= 4096 ? kHop8Wide : kHop8FewRows;
+    }
     if (lda >= (1ll << 23)) return M >= 6144 ? kHopLongRows : kHopFewRows;  // rows of >= 8 M columns
     if (M >= 16384) return K <= 1024 ? kSeqShortRows : K >= 65536 ? kHopLongRows : kSeqManyRows;
     if (M >= 12288) return kSeqMidRows;

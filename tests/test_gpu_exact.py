@@ -33,6 +33,12 @@ def signed(A, seed):
     return A * rng.choice([-1.0, 1.0], size=A.shape)
 
 
+def needs_16b(name):
+    """16-B loads (LDS-DMA or plain): 16-B aligned A and x and an even lda; `hop8_*` (8-B loads),
+    `seq_scalar` and `auto` take anything."""
+    return name.startswith(("seq_r", "seqx_", "hop_"))
+
+
 def exact_variants():
     lib = _lib.lib
     return [(v, lib.mvg_gemv_exact_variant_name(v).decode()) for v in range(lib.mvg_gemv_exact_variant_count())]
@@ -44,7 +50,7 @@ def test_gemv_exact_every_variant_is_the_reference_sum(m, k):
     x = signed(oracle.synth(1, k, 4242)[0], k)
     want = oracle.multiply_std_rowwise(A, x)
     for v, name in exact_variants():
-        if name not in ("auto", "seq_scalar") and k % 2:  # the 16-B forms need an even lda
+        if needs_16b(name) and k % 2:  # the 16-B forms need an even lda
             with pytest.raises(_lib.MvgError):
                 mm.multiply_std_rowwise(A, x, variant=v, exact=True)
             continue
@@ -53,19 +59,22 @@ def test_gemv_exact_every_variant_is_the_reference_sum(m, k):
 
 
 def test_gemv_exact_hop_segment_edges():
-    # the chain-hopping forms (hop_l<L>_w<W>_u<U>): a segment is S = L*W columns and U segments
+    # the chain-hopping forms (hop_l<L>_w<W>_u<U>, hop8_* with 8-B loads): a segment is S = L*W columns and U segments
     # are in flight; after an odd number of segments the chain ends in lane L-1, after an even
     # number in lane 0, so every variant is run with odd and even segment counts, with and
     # without leftover segments (nseg % U), a column tail, no whole segment at all, and a
     # last wave with rows to spare
     for v, name in exact_variants():
-        if not name.startswith("hop_"):
+        if not name.startswith("hop"):
             continue
         L, W, U = (int(part[1:]) for part in name.split("_")[1:4])
         S = L * W
         m = 3 * (64 // L) + 1
-        for k in (S - 2, S, 3 * S + 2, (U + 1) * S, (U + 1) * S + 2, (U + 2) * S, 2 * U * S, 2 * U * S + 2,
-                  (3 * U - 1) * S):
+        ks = [S - 2, S, 3 * S + 2, (U + 1) * S, (U + 1) * S + 2, (U + 2) * S, 2 * U * S, 2 * U * S + 2,
+              (3 * U - 1) * S]
+        if not needs_16b(name):  # odd widths too: every other row starts 8 bytes off a 16-B boundary
+            ks += [k + 1 for k in ks]
+        for k in ks:
             A = signed(oracle.synth(m, k, 42), k)
             x = signed(oracle.synth(1, k, 4242)[0], k + 1)
             y = mm.multiply_std_rowwise(A, x, variant=v, exact=True)
