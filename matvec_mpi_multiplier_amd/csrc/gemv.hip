@@ -14,8 +14,10 @@
 // so the result is deterministic run to run. LPR = 64 serves long rows (K >= ~1024),
 // LPR = 16/8 serves short rows (the 4,194,304 x 512 tall-skinny config) without idle lanes.
 //
-// A row stride (lda) that is odd, or a misaligned base, cannot use 16-B loads: the scalar
-// variant (8 B per lane, still coalesced) covers it.
+// A row stride (lda) that is odd, or a base 8 bytes off a 16-B boundary, still takes the 16-B
+// kernels: their loads promise only 8-B alignment (dbl2u below) and compile to the same
+// global_load_dwordx4, which gfx950 serves unaligned. Only a base off an 8-B boundary falls back
+// to the scalar variants (8 B per lane, still coalesced).
 #include "common.h"
 
 #include <map>
@@ -25,13 +27,17 @@
 namespace mvg {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+// the same pair as a load type promising only 8-B alignment: still one global_load_dwordx4
+// (gfx950 serves unaligned vector loads), so the 16-B kernels also run on an odd lda or a view
+// 8 bytes off a 16-B boundary, with no 16-B alignment assumed anywhere in the address code
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
 
 template <bool NT>
 __device__ __forceinline__ dbl2 load2(const double* p) {
     if constexpr (NT) {
-        return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
+        return __builtin_nontemporal_load(reinterpret_cast<const dbl2u*>(p));
     } else {
-        return *reinterpret_cast<const dbl2*>(p);
+        return *reinterpret_cast<const dbl2u*>(p);
     }
 }
 
@@ -117,7 +123,7 @@ __device__ __forceinline__ void fma_chunk(double (&acc)[RPG], const dbl2 (&xv)[U
         }
 }
 
-// 16-B path. Requires lda even, A and x 16-B aligned.
+// 16-B path (A and x 8-B aligned; fastest with an even lda and 16-B aligned A, x).
 template <int LPR, int RPG, int UNR, bool NT, int OPT>
 __global__ __launch_bounds__(kBlock) void gemv_vec(const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ x,
@@ -582,11 +588,13 @@ constexpr int kRowSmall = variant_id(kVariants, "rowblk_w2_r2_u4");
 constexpr int kVecTwoRows = variant_id(kVariants, "vec_l64_r2_u4_nt1_o7");
 constexpr int kVecFourRows = variant_id(kVariants, "vec_l64_r4_u4_nt1_o5");
 constexpr int kVecOneRow = variant_id(kVariants, "vec_l64_r1_u4_nt1_o5");
+constexpr int kRowLongOdd = variant_id(kVariants, "rowblk_w4_r2_u8_xcd");
+constexpr int kVecFourRowsOdd = variant_id(kVariants, "vec_l64_r4_u4_nt1_o0");
 static_assert(kScalarLong > 0 && !kVariants[kScalarLong].vec, "8-B fallback must not need 16-B loads");
 static_assert(kScalarShort > 0 && !kVariants[kScalarShort].vec, "8-B fallback must not need 16-B loads");
 static_assert(kSplitK > 0 && kVariants[kSplitK].split != nullptr, "split-K variant");
 static_assert(kRowLong > 0 && kRowMid > 0 && kRowSmall > 0 && kVecTwoRows > 0 && kVecFourRows > 0 &&
-                  kVecOneRow > 0,
+                  kVecOneRow > 0 && kRowLongOdd > 0 && kVecFourRowsOdd > 0,
               "dispatch names a variant missing from kVariants");
 
 constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4 per CU)
@@ -613,9 +621,19 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 // The wave-owns-rows picks finish with DPP sums (kDpp, round 2): within +-0.3 % of the
 // ds_bpermute forms on every swept shape (profiles/r02/variant_sweep_dpp.jsonl) — the
 // reduction was never the limit — and they keep the LDS unit out of the epilogue.
-static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
+// An odd lda or a view 8 bytes off a 16-B boundary (round 2: the 16-B kernels read through
+// unaligned vector loads, variant_sweep21_odd.jsonl over 8 odd-width shapes): split-K for few
+// long rows, else the XCD-remapped long-row form (rows alternate between 16-B aligned and not,
+// and per-XCD contiguous streams win there: 16384 x 16383 307 us, 65536 x 8191 609 us, against
+// 329 / 652 for the 8-B kernel); the 2-wave row form for 768 < K < 4096, wave-owns-4-rows for
+// short rows. Only operands off an 8-B boundary keep the 8-B kernels.
+static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool aligned8) {
     const bool vec = aligned && (lda % 2 == 0);
-    if (!vec) return K >= 256 ? kScalarLong : kScalarShort;
+    if (!vec) {
+        if (!aligned8) return K >= 256 ? kScalarLong : kScalarShort;
+        if (K >= 4096) return (M + 1) / 2 < 700 ? kSplitK : kRowLongOdd;
+        return K > 768 ? kRowSmall : kVecFourRowsOdd;
+    }
     const int64_t nrb = (M + 1) / 2;
     if (K >= 8192) {
         if (nrb < 700) return kSplitK;
@@ -1256,7 +1274,7 @@ extern "C" {
 
 int mvg_gemv_variant_count(void) { return kNumVariants; }
 
-int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k) { return pick_variant(lda, m, k, true); }
+int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k) { return pick_variant(lda, m, k, true, true); }
 
 const char* mvg_gemv_variant_name(int v) {
     if (v < 0 || v >= kNumVariants) return "invalid";
@@ -1279,9 +1297,10 @@ int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, i
     if (!A || !x) return fail(MVG_E_INVALID, "mvg_gemv: null A or x");
     if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv: lda < k");
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
-    int v = variant == 0 ? pick_variant(lda, m, k, aligned) : variant;
-    if (kVariants[v].vec && !(aligned && lda % 2 == 0))
-        return fail(MVG_E_INVALID, "mvg_gemv: 16-B variant needs even lda and 16-B aligned A, x");
+    const bool aligned8 = ((uintptr_t)A % 8 == 0) && ((uintptr_t)x % 8 == 0);
+    int v = variant == 0 ? pick_variant(lda, m, k, aligned, aligned8) : variant;
+    if (kVariants[v].vec && ((uintptr_t)A % 8 != 0 || (uintptr_t)x % 8 != 0))
+        return fail(MVG_E_INVALID, "mvg_gemv: 16-B variant needs 8-B aligned A, x");
     return launch(v, A, lda, x, y, m, k, s, variant != 0);
 }
 

@@ -48,12 +48,24 @@ def test_gemv_all_variants_vs_oracle(m, k):
     y_ref = oracle.multiply_std_rowwise(A, x)
     for v in range(_lib.lib.mvg_gemv_variant_count()):
         name = _lib.lib.mvg_gemv_variant_name(v).decode()
-        if name.startswith(("vec", "rowblk")) and k % 2:
-            with pytest.raises(_lib.MvgError):
-                mm.multiply_std_rowwise(A, x, variant=v)
-            continue
+        # an odd k is an odd lda here: the 16-B kernels read every other row 8 bytes off a
+        # 16-B boundary (unaligned vector loads) and must give the same result
         y = mm.multiply_std_rowwise(A, x, variant=v)
         assert max_rel(y, y_ref) <= TOL, (name, m, k)
+
+
+def test_gemv_16b_kernels_on_views_off_16b():
+    # A and x starting 8 bytes into their buffers (an offset view), odd and even lda
+    for m, k, lda in [(70, 300, 301), (130, 4096, 4097), (9, 20001, 20002), (257, 1000, 1000)]:
+        full = oracle.synth(m, lda + 1, 42)
+        x = oracle.synth(1, k + 1, 4242)[0]
+        dA, dx, dy = mm.DeviceBuffer(m * (lda + 1)).upload(full), mm.DeviceBuffer(k + 1).upload(x), mm.DeviceBuffer(m)
+        view = full.reshape(-1)[1 + np.arange(m)[:, None] * lda + np.arange(k)[None, :]]  # rows at 8 + lda*8*r
+        want = oracle.multiply_std_rowwise(view, x[1:k + 1])
+        for v in range(_lib.lib.mvg_gemv_variant_count()):
+            mm.gemv(dA.ptr + 8, lda, dx.ptr + 8, dy.ptr, m, k, None, v)
+            _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
+            assert max_rel(dy.download(), want) <= TOL, (_lib.lib.mvg_gemv_variant_name(v).decode(), m, k, lda)
 
 
 def test_gemv_padded_lda_and_offsets():
