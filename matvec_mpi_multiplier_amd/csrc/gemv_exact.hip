@@ -468,6 +468,7 @@ static constexpr SeqVariant kSeqVariants[] = {
     HOP(8, 2, 24),
     HOP(4, 4, 8),
     HOP(4, 2, 16),
+    HOP(32, 16, 4),  // 128-B runs per lane between hops: the fewest rows (sweep_exact12_w16.jsonl)
     // the same with 8-B loads: any alignment, any lda
     HOP8(8, 2, 16),
     HOP8(8, 2, 24),
@@ -501,6 +502,7 @@ constexpr int kHopRows = seq_id(kSeqVariants, "hop_l8_w2_u16");
 constexpr int kHopLongRows = seq_id(kSeqVariants, "hop_l8_w2_u24");
 constexpr int kHopWide = seq_id(kSeqVariants, "hop_l16_w4_u8");
 constexpr int kHopFewRows = seq_id(kSeqVariants, "hop_l32_w8_u4");
+constexpr int kHopFewestRows = seq_id(kSeqVariants, "hop_l32_w16_u4");
 // 8-B-load counterparts: any alignment, any lda
 constexpr int kHop8TallRows = seq_id(kSeqVariants, "hop8_l16_w2_u16");
 constexpr int kHop8Rows = seq_id(kSeqVariants, "hop8_l8_w2_u16");
@@ -515,7 +517,7 @@ static_assert(kSeqVariants[kHopRows].needs == kVec16 && kSeqVariants[kHopLongRow
                   kSeqVariants[kHopFewRows].needs == kVec16,
               "the dispatch's choice for lda >= 2^23 must not need 32-bit LDS offsets");
 static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRows > 0 && kHopLongRows > 0 &&
-                  kHopWide > 0 && kHopFewRows > 0,
+                  kHopWide > 0 && kHopFewRows > 0 && kHopFewestRows > 0,
               "exact dispatch names a missing variant");
 
 // From the round-2 MI355X sweeps (tools/sweep_exact.py -> profiles/r02/sweep_exact*.jsonl; the
@@ -527,7 +529,8 @@ static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRo
 // reference's R x 60000 shapes — by how many lanes share a row: 8 lanes x 16 B per row where
 // >= 6144 rows (or K <= 8192) give enough waves, 16 lanes x 32 B for 2048 .. 6143 rows,
 // 32 lanes x 64 B for fewer rows with K > 4096 (the chain dominates: longer runs per lane
-// between hops), 16 x 32 B for short ones. An odd lda or operands off a 16-B boundary take the
+// between hops; 32 x 128 B below 512 rows, 120 x 60000 in 162 instead of 183 us), 16 x 32 B for
+// short ones. An odd lda or operands off a 16-B boundary take the
 // same forms with 8-B loads (hop8_*; 16 lanes per row from 12288 rows: sweep_exact11_hop8.jsonl,
 // 2-36x faster than the lane-per-row 8-B kernel seq_scalar on odd widths).
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
@@ -542,7 +545,8 @@ static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
     if (M >= 12288) return kSeqMidRows;
     if (M >= 6144) return kHopRows;
     if (M >= 2048) return K <= 8192 ? kHopRows : kHopWide;
-    return K <= 4096 ? kHopWide : kHopFewRows;
+    if (K <= 4096) return kHopWide;
+    return M < 512 ? kHopFewestRows : kHopFewRows;
 }
 
 }  // namespace mvg
