@@ -1325,10 +1325,11 @@ int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_
         return fail(MVG_E_INVALID, "mvg_gemv_multi: null pointer or leading dimension too small");
     hipStream_t s = (hipStream_t)stream;
     const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)X % 16 == 0) && lda % 2 == 0 && ldx % 2 == 0;
-    if (!vec || k == 0) {  // the 8-B path (or k = 0): one vector at a time
+    if (!vec || k == 0) {  // odd lda/ldx or a view off 16 B (or k = 0): one vector at a time,
+        // each through the single-vector dispatch (its unaligned 16-B forms, §4 "Odd widths")
         if (variant != 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: variants need even lda/ldx, 16-B aligned A, X");
         for (int v = 0; v < nv; ++v) {
-            int rc = mvg_gemv_variant(A, lda, X + v * ldx, Y + v * ldy, m, k, vec ? 0 : kScalarLong, stream);
+            int rc = mvg_gemv_variant(A, lda, X + v * ldx, Y + v * ldy, m, k, 0, stream);
             if (rc != MVG_OK) return rc;
         }
         return MVG_OK;
