@@ -176,11 +176,10 @@ const char* mvg_gemv_multi_variant_name(int variant);
  *   sum = 0; for j < k: sum = round(sum + round(A[i*lda + j] * x[j]))
  * (src/matr_utils.c:87-93: a rounded multiply then a rounded add, left to right, no FMA), so
  * y is bit-identical to multiply_std_rowwise on the same inputs (and to the strip sums of
- * multiply_colwise, src/multiplier_colwise.c:107-122). Tall shapes: one lane per row, rows
- * streamed through LDS; fewer rows (< 12288) or K >= 65536: several lanes per row, the running
- * sum handed lane to lane in column order (csrc/gemv_exact.hip). Any lda >= k and alignment
- * (16-B aligned A, x with an even lda take the 16-B paths — the LDS ones only for lda < 2^23 —
- * anything else the lane-sharing forms with 8-B loads). */
+ * multiply_colwise, src/multiplier_colwise.c:107-122). Tall shapes whose rows start on 128-B
+ * lines: one lane per row, rows streamed through LDS; everything else: several lanes per row,
+ * the running sum handed lane to lane in column order (csrc/gemv_exact.hip). Any lda >= k and
+ * any alignment. */
 int mvg_gemv_exact(const double* d_A, int64_t lda, const double* d_x, double* d_y,
                    int64_t m, int64_t k, void* stream);
 /* The reference's in-process call on host pointers, src/matr_utils.h:4-10:

@@ -29,9 +29,10 @@
 // With RW < 64 the upper lanes repeat rows and store nothing (more waves for few rows).
 // Rows past M re-read row M-1 (never stored); the column tail K % 2T and any A that is not
 // 16-B aligned with an even lda take per-lane 8-B loads in the same column order.
-// With fewer rows (< 12288) or very long ones (K >= 65536) the chain-hopping forms
-// (gemv_seq_hop, below) take over: L lanes share a row, the data arrives by plain coalesced
-// loads into VGPRs, and the running sum hops from lane to lane by DPP, still in column order.
+// Everywhere but line-aligned tall shapes (>= 32768 rows, lda a multiple of 16, 2048 < K <
+// 65536) the chain-hopping forms (gemv_seq_hop, below) take over: L lanes share a row, the data
+// arrives by plain coalesced loads into VGPRs, and the running sum hops from lane to lane by
+// DPP, still in column order.
 #include "common.h"
 
 // hipcc contracts a*b + c into an FMA by default (-ffp-contract=fast); the reference rounds the
@@ -302,6 +303,30 @@ __device__ __forceinline__ void load_run(const double* p, dbl2x (&d)[V]) {
     }
 }
 
+// A segment whose columns outside [lo, hi) contribute 0 x 0 = +0.0 products: adding +0.0 leaves
+// the running sum unchanged bit for bit (it is never -0.0: it starts at +0.0 and
+// round-to-nearest gives +0.0 for every exact cancellation). cb: this lane's first column.
+template <int L, int W>
+__device__ __forceinline__ double hop_masked_segment(double sum, const double* __restrict__ arow,
+                                                     const double* __restrict__ x, int64_t cb, int64_t lo,
+                                                     int64_t hi, bool fwd) {
+    dbl2x ta[W / 2], tx[W / 2];
+#pragma unroll
+    for (int v = 0; v < W / 2; ++v) {
+        const int64_t j0 = cb + 2 * v, j1 = j0 + 1;
+        const bool in0 = j0 >= lo && j0 < hi, in1 = j1 >= lo && j1 < hi;
+        ta[v] = dbl2x{in0 ? arow[j0] : 0.0, in1 ? arow[j1] : 0.0};
+        tx[v] = dbl2x{in0 ? x[j0] : 0.0, in1 ? x[j1] : 0.0};
+    }
+    return fwd ? hop_segment<L, W, true>(sum, ta, tx) : hop_segment<L, W, false>(sum, ta, tx);
+}
+
+// Segment g of a row runs forward (lane 0 -> L-1) when g is even. A row's segments: a head
+// (g = 0) ending at the row's first 128-B boundary, so that every main segment's loads start on
+// a cache line — a row that starts mid-line would make each 128-B piece touch two lines
+// (16384 x 16386: 373 us against 314 us at 16384^2, sweep_exact13_lines.jsonl) — then nseg
+// main segments, the same count for every row of the wave, then one or two tail segments for
+// what is left. Head and tails are masked segments (zeros outside the row's columns).
 template <int L, int W, int U, bool B8 = false>
 __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ x,
@@ -311,48 +336,61 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
     constexpr int R = 64 / L;  // rows per wave
     constexpr int S = L * W;   // columns per segment
     constexpr int V = W / 2;   // 16-B pieces per lane per segment
+    static_assert(S >= 16, "the head (up to 15 columns) fits one segment");
     const int lane = threadIdx.x;
     const int c = lane % L;
     const int64_t row = (int64_t)blockIdx.x * R + lane / L;
     const int64_t rr = row < M ? row : M - 1;
     const double* arow = A + rr * lda;
-    const int64_t nseg = K / S;
     const int off[2] = {c * W, (L - 1 - c) * W};  // even / odd segment
-
     double sum = 0.0;
-    if (nseg > 0) {
-        dbl2x a[U][V], xv[U][V];
-#pragma unroll
-        for (int i = 0; i < U; ++i) {
-            const int64_t s = i < nseg ? i : nseg - 1;
-            load_run<V, B8, true>(arow + s * S + off[i & 1], a[i]);
-            load_run<V, B8, false>(x + s * S + off[i & 1], xv[i]);
-            __builtin_amdgcn_sched_barrier(0);  // same load order as the loop's refills
-        }
-        // Whole groups of U segments, one basic block: slot i is summed, then refilled U segments
-        // ahead; the scheduling barriers keep the loads in slot order, so the compiler's vmcnt
-        // waits retire exactly the slot about to be summed.
-        int64_t base = 0;
-        for (; base + U <= nseg; base += U) {
+    int64_t nseg = 0, ntail = 0;
+    if (K > 0) {
+        // head: columns [0, h) with h the distance to the row's next 128-B boundary (0 ... 15)
+        const int64_t h = (int64_t)(((128u - ((uintptr_t)arow & 127u)) & 127u) >> 3);
+        sum = hop_masked_segment<L, W>(sum, arow, x, h - S + off[0], 0, h < K ? h : K, true);
+        nseg = K >= 15 ? (K - 15) / S : 0;            // every row has >= nseg * S columns past its head
+        ntail = (K - nseg * S + S - 1) / S;            // the most any row has left: 1 or 2 segments
+        const double* ar = arow + h;
+        const double* xr = x + h;
+        if (nseg > 0) {
+            dbl2x a[U][V], xv[U][V];
 #pragma unroll
             for (int i = 0; i < U; ++i) {
-                sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
-                __builtin_amdgcn_sched_barrier(0);
-                const int64_t s = base + i + U < nseg ? base + i + U : nseg - 1;
-                load_run<V, B8, true>(arow + s * S + off[i & 1], a[i]);
-                load_run<V, B8, false>(x + s * S + off[i & 1], xv[i]);
-                __builtin_amdgcn_sched_barrier(0);
+                const int64_t sg = i < nseg ? i : nseg - 1;
+                load_run<V, B8, true>(ar + sg * S + off[(i + 1) & 1], a[i]);
+                load_run<V, true, false>(xr + sg * S + off[(i + 1) & 1], xv[i]);
+                __builtin_amdgcn_sched_barrier(0);  // same load order as the loop's refills
             }
-        }
-        // the last nseg % U segments are already in slots 0 .. nseg % U - 1 (base is even)
+            // Whole groups of U segments, one basic block: slot i is summed, then refilled U
+            // segments ahead; the scheduling barriers keep the loads in slot order, so the
+            // compiler's vmcnt waits retire exactly the slot about to be summed. Main segment i
+            // is the row's segment i + 1 (after the head).
+            int64_t base = 0;
+            for (; base + U <= nseg; base += U) {
 #pragma unroll
-        for (int i = 0; i < U; ++i)
-            if (base + i < nseg)
-                sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
+                for (int i = 0; i < U; ++i) {
+                    sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int64_t sg = base + i + U < nseg ? base + i + U : nseg - 1;
+                    load_run<V, B8, true>(ar + sg * S + off[(i + 1) & 1], a[i]);
+                    load_run<V, true, false>(xr + sg * S + off[(i + 1) & 1], xv[i]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            // the last nseg % U segments are already in slots 0 .. nseg % U - 1 (base is even)
+#pragma unroll
+            for (int i = 0; i < U; ++i)
+                if (base + i < nseg)
+                    sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
+        }
+        for (int64_t t = 0; t < ntail; ++t) {
+            const int64_t g = 1 + nseg + t;  // the row's segment index
+            sum = hop_masked_segment<L, W>(sum, arow, x, h + (nseg + t) * S + off[g & 1], h, K, (g & 1) == 0);
+        }
     }
-    // the chain ends in lane L-1 after an even-numbered last segment, in lane 0 otherwise
-    const int holder = (nseg & 1) ? L - 1 : 0;
-    for (int64_t j = nseg * S; j < K; ++j) sum = seq_step(sum, arow[j], x[j]);
+    // the chain ends in lane L-1 after an odd number of segments, in lane 0 otherwise
+    const int holder = (K > 0 && ((1 + nseg + ntail) & 1)) ? L - 1 : 0;
     if (c == holder && row < M) y[row] = sum;
 }
 
@@ -467,14 +505,13 @@ static constexpr SeqVariant kSeqVariants[] = {
     HOP(8, 2, 16),
     HOP(8, 2, 24),
     HOP(4, 4, 8),
-    HOP(4, 2, 16),
-    HOP(32, 16, 4),  // 128-B runs per lane between hops: the fewest rows (sweep_exact12_w16.jsonl)
     // the same with 8-B loads: any alignment, any lda
     HOP8(8, 2, 16),
     HOP8(8, 2, 24),
     HOP8(8, 4, 8),
     HOP8(16, 2, 16),
     HOP8(16, 4, 8),
+    HOP8(16, 8, 4),
     HOP8(32, 8, 4),
 };
 constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
@@ -495,58 +532,40 @@ constexpr int seq_id(const SeqVariant (&table)[N], const char* name) {
     return -1;
 }
 constexpr int kSeqScalar = seq_id(kSeqVariants, "seq_scalar");
-constexpr int kSeqShortRows = seq_id(kSeqVariants, "seqx_r64_t32_b2_g8");
 constexpr int kSeqManyRows = seq_id(kSeqVariants, "seqx_r64_t16_b2_g8");
-constexpr int kSeqMidRows = seq_id(kSeqVariants, "seqx_r32_t64_b2_g16");
-constexpr int kHopRows = seq_id(kSeqVariants, "hop_l8_w2_u16");
-constexpr int kHopLongRows = seq_id(kSeqVariants, "hop_l8_w2_u24");
-constexpr int kHopWide = seq_id(kSeqVariants, "hop_l16_w4_u8");
-constexpr int kHopFewRows = seq_id(kSeqVariants, "hop_l32_w8_u4");
-constexpr int kHopFewestRows = seq_id(kSeqVariants, "hop_l32_w16_u4");
-// 8-B-load counterparts: any alignment, any lda
-constexpr int kHop8TallRows = seq_id(kSeqVariants, "hop8_l16_w2_u16");
-constexpr int kHop8Rows = seq_id(kSeqVariants, "hop8_l8_w2_u16");
-constexpr int kHop8Wide = seq_id(kSeqVariants, "hop8_l16_w4_u8");
-constexpr int kHop8FewRows = seq_id(kSeqVariants, "hop8_l32_w8_u4");
+constexpr int kHopRows = seq_id(kSeqVariants, "hop8_l8_w2_u16");
+constexpr int kHopLongRows = seq_id(kSeqVariants, "hop8_l8_w2_u24");
+constexpr int kHopWide = seq_id(kSeqVariants, "hop8_l16_w4_u8");
+constexpr int kHopWidest = seq_id(kSeqVariants, "hop8_l16_w8_u4");
+constexpr int kHopFewRows = seq_id(kSeqVariants, "hop8_l32_w8_u4");
 static_assert(kSeqScalar > 0 && kSeqVariants[kSeqScalar].needs == kAnyOperands, "8-B exact fallback");
-static_assert(kHop8TallRows > 0 && kHop8Rows > 0 && kHop8Wide > 0 && kHop8FewRows > 0 &&
-                  kSeqVariants[kHop8TallRows].needs == kAnyOperands && kSeqVariants[kHop8Rows].needs == kAnyOperands &&
-                  kSeqVariants[kHop8Wide].needs == kAnyOperands && kSeqVariants[kHop8FewRows].needs == kAnyOperands,
-              "the dispatch's choice for any operands must take any operands");
-static_assert(kSeqVariants[kHopRows].needs == kVec16 && kSeqVariants[kHopLongRows].needs == kVec16 &&
-                  kSeqVariants[kHopFewRows].needs == kVec16,
-              "the dispatch's choice for lda >= 2^23 must not need 32-bit LDS offsets");
-static_assert(kSeqShortRows > 0 && kSeqManyRows > 0 && kSeqMidRows > 0 && kHopRows > 0 && kHopLongRows > 0 &&
-                  kHopWide > 0 && kHopFewRows > 0 && kHopFewestRows > 0,
+static_assert(kSeqManyRows > 0 && kHopRows > 0 && kHopLongRows > 0 && kHopWide > 0 && kHopWidest > 0 &&
+                  kHopFewRows > 0,
               "exact dispatch names a missing variant");
+static_assert(kSeqVariants[kHopRows].needs == kAnyOperands && kSeqVariants[kHopLongRows].needs == kAnyOperands &&
+                  kSeqVariants[kHopWide].needs == kAnyOperands && kSeqVariants[kHopWidest].needs == kAnyOperands &&
+                  kSeqVariants[kHopFewRows].needs == kAnyOperands,
+              "the chain-hopping picks take any operands");
 
 // From the round-2 MI355X sweeps (tools/sweep_exact.py -> profiles/r02/sweep_exact*.jsonl; the
-// dispatch below from sweep_exact9_hop.jsonl, 23 shapes from 600^2 to 131072^2 and
-// 4194304 x 512). Tall shapes keep the LDS forms — >= 16384 rows, 64-row waves (512-B row
-// segments for short rows, K <= 1024; 256-B ones otherwise), 12288 .. 16383 rows 32-row waves
-// with 1-KiB segments — except for very long rows (K >= 65536: 65536^2 and 131072^2, 2-6 %
-// faster with 8 lanes per row and 24 segments in flight). Below that the chain-hopping register forms win — up to 3.2x on the
-// reference's R x 60000 shapes — by how many lanes share a row: 8 lanes x 16 B per row where
-// >= 6144 rows (or K <= 8192) give enough waves, 16 lanes x 32 B for 2048 .. 6143 rows,
-// 32 lanes x 64 B for fewer rows with K > 4096 (the chain dominates: longer runs per lane
-// between hops; 32 x 128 B below 512 rows, 120 x 60000 in 162 instead of 183 us), 16 x 32 B for
-// short ones. An odd lda or operands off a 16-B boundary take the
-// same forms with 8-B loads (hop8_*; 16 lanes per row from 12288 rows: sweep_exact11_hop8.jsonl,
-// 2-36x faster than the lane-per-row 8-B kernel seq_scalar on odd widths).
-static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned) {
-    if (!operands_ok(kVec16, lda, aligned)) {  // odd lda or operands off 16 B: the 8-B-load forms
-        if (M >= 12288) return kHop8TallRows;
-        if (M >= 6144) return kHop8Rows;
-        if (M >= 2048) return K <= 8192 ? kHop8Rows : kHop8Wide;
-        return K <= 4096 ? kHop8Wide : kHop8FewRows;
-    }
-    if (lda >= (1ll << 23)) return M >= 6144 ? kHopLongRows : kHopFewRows;  // rows of >= 8 M columns
-    if (M >= 16384) return K <= 1024 ? kSeqShortRows : K >= 65536 ? kHopLongRows : kSeqManyRows;
-    if (M >= 12288) return kSeqMidRows;
-    if (M >= 6144) return kHopRows;
-    if (M >= 2048) return K <= 8192 ? kHopRows : kHopWide;
-    if (K <= 4096) return kHopWide;
-    return M < 512 ? kHopFewestRows : kHopFewRows;
+// dispatch below from sweep_exact13_lines.jsonl, 31 shapes: the BASELINE configs' shards, the
+// reference's own sizes, odd widths and rows that start mid-line). The LDS forms only where
+// they still win: >= 32768 rows whose every row starts on a 128-B line (A on a line, lda a
+// multiple of 16) with 2048 < K < 65536 — 64-row waves of 256-B row segments (the strips and
+// blocks of configs 3 and 4: 622 against 663 us, 2461 against 2490). Everything else takes the
+// chain-hopping forms, with 8-B loads (they equal the 16-B ones on aligned data and take any
+// lda): 8 lanes x 16 B per row from 6144 rows (or K <= 8192; 24 segments in flight for
+// K >= 65536), 16 lanes x 32 B for 2048 .. 6143 rows (x 64 B below 4096 rows with K >= 32768),
+// 32 lanes x 64 B for fewer rows with K > 4096, where the chain dominates (the reference's
+// R x 60000: 1200 rows in 203 us, 679 with the LDS forms), 16 x 32 B for short ones. On rows
+// that start mid-line they beat the tree form itself (16384 x 16386: 305 us against 315);
+// config 5's shards and 4,194,304 x 512 run at 0.98-0.99 of the tree form's speed.
+static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
+    if (lines && operands_ok(kVec16Lda23, lda, aligned) && M >= 32768 && K > 2048 && K < 65536)
+        return kSeqManyRows;
+    if (M >= 6144) return K >= 65536 ? kHopLongRows : kHopRows;
+    if (M >= 2048) return K <= 8192 ? kHopRows : M < 4096 && K >= 32768 ? kHopWidest : kHopWide;
+    return K <= 4096 ? kHopWide : kHopFewRows;
 }
 
 }  // namespace mvg
@@ -562,7 +581,9 @@ const char* mvg_gemv_exact_variant_name(int v) {
     return kSeqVariants[v].name;
 }
 
-int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k) { return pick_seq_variant(lda, m, k, true); }
+int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k) {
+    return pick_seq_variant(lda, m, k, true, lda % 16 == 0);
+}
 
 int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
                            int variant, void* stream) {
@@ -577,7 +598,8 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv_exact: lda < k");
     }
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
-    const int v = variant == 0 ? pick_seq_variant(lda, m, k, aligned) : variant;
+    const bool lines = (uintptr_t)A % 128 == 0 && lda % 16 == 0;  // every row starts on a 128-B line
+    const int v = variant == 0 ? pick_seq_variant(lda, m, k, aligned, lines) : variant;
     if (!operands_ok(kSeqVariants[v].needs, lda, aligned))
         return fail(MVG_E_INVALID, kSeqVariants[v].needs == kVec16
                                        ? "mvg_gemv_exact: 16-B variant needs 16-B aligned A, x and an even lda"

@@ -49,6 +49,10 @@ SHAPES = [
     ("odd_1200x60001", 1200, 60001),
     ("odd_65536x8191", 65536, 8191),
     ("odd_4096x16383", 4096, 16383),
+    # even widths whose rows are 16-B but not 128-B aligned (row stride 131088 / 131104 B)
+    ("even_16384x16386", 16384, 16386),
+    ("even_16384x16388", 16384, 16388),
+    ("even_16384x16400", 16384, 16400),
 ]
 
 
