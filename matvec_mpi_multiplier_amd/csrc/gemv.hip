@@ -315,6 +315,95 @@ __global__ __launch_bounds__(NW * 64) void gemv_rowblock(const double* __restric
     }
 }
 
+// Row-per-workgroup form for rows that do not start on 128-B lines (an lda that is not a
+// multiple of 16 — the reference's 4200 and 10200, every odd width — or a view off a line):
+// there each 1-KiB wave load spans 9 cache lines instead of 8 (7 % more L2 requests at
+// 16384 x 16386, profiles/r02/pmc_exact_gemv_seq_hop_final_16384x16386.json). Rows r and r + p
+// with p = 16 >> min(ctz(lda), 4) start at the same offset within a line (p * lda * 8 is a
+// multiple of 128), so a workgroup takes that pair: both rows first add their h columns up to
+// the next line (h the same for both, 0 ... 15 columns, lanes 0 .. h-1 of wave 0), then stream
+// line-aligned chunks against x shifted by the same h — x stays one load for both rows, as in
+// gemv_rowblock. Workgroup b of a block of 2p rows takes rows (b mod p, b mod p + p): the pairs
+// of a block cover it, consecutive workgroups still read neighbouring rows.
+template <int NW, int UNR, bool NT, int XCD = 0>
+__global__ __launch_bounds__(NW * 64) void gemv_rowblock_lines(const double* __restrict__ A, int64_t lda,
+                                                               const double* __restrict__ x,
+                                                               double* __restrict__ y, int64_t M,
+                                                               int64_t K) {
+    constexpr int RPB = 2;
+    __shared__ double part[NW][RPB];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    int64_t bid = blockIdx.x;
+    if constexpr (XCD == 1) bid = xcd_remap(bid, gridDim.x);
+    const int tz = lda == 0 ? 4 : __builtin_ctzll((unsigned long long)lda);
+    const int64_t p = 16 >> (tz < 4 ? tz : 4);
+    const int64_t row_of[RPB] = {bid / p * 2 * p + bid % p, bid / p * 2 * p + bid % p + p};
+    const double* arow[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) arow[r] = A + (row_of[r] < M ? row_of[r] : M - 1) * lda;
+    int64_t h = (int64_t)(((128u - ((uintptr_t)arow[0] & 127u)) & 127u) >> 3);
+    h = h < K ? h : K;
+    double acc[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) acc[r] = threadIdx.x < h ? arow[r][threadIdx.x] * x[threadIdx.x] : 0.0;
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) arow[r] += h;
+    const double* xs = x + h;
+    const int64_t Kh = K - h;
+
+    constexpr int64_t kStep = 128;
+    constexpr int64_t kChunk = kStep * UNR;
+    const int64_t nch = Kh / kChunk;
+    const int64_t c0 = 2 * lane;
+    int64_t i = w;
+    if (i < nch) {
+        dbl2 xa[UNR], xb[UNR];
+        dbl2 aa[RPB][UNR], ab[RPB][UNR];
+        load_chunk<RPB, UNR, NT>(arow, xs, i * kChunk + c0, kStep, xa, aa);
+        for (; i + NW < nch; i += 2 * NW) {
+            load_chunk<RPB, UNR, NT>(arow, xs, (i + NW) * kChunk + c0, kStep, xb, ab);
+            fma_chunk<RPB, UNR>(acc, xa, aa);
+            if (i + 2 * NW < nch) {
+                load_chunk<RPB, UNR, NT>(arow, xs, (i + 2 * NW) * kChunk + c0, kStep, xa, aa);
+                fma_chunk<RPB, UNR>(acc, xb, ab);
+            } else {
+                fma_chunk<RPB, UNR>(acc, xb, ab);
+                i = nch;
+                break;
+            }
+        }
+        if (i < nch) fma_chunk<RPB, UNR>(acc, xa, aa);
+    }
+    for (int64_t c = nch * kChunk + 2 * (int64_t)threadIdx.x; c < Kh; c += 2 * NW * 64) {
+        if (c + 1 < Kh) {
+            const dbl2 xv = load2<false>(xs + c);
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) {
+                const dbl2 a = load2<NT>(arow[r] + c);
+                acc[r] = __builtin_fma(a.x, xv.x, acc[r]);
+                acc[r] = __builtin_fma(a.y, xv.y, acc[r]);
+            }
+        } else {
+            const double xv = xs[c];
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) acc[r] = __builtin_fma(arow[r][c], xv, acc[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        const double s = group_sum_dpp<64>(acc[r]);
+        if (lane == 0) part[w][r] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < RPB && row_of[threadIdx.x] < M) {
+        double s = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += part[v][threadIdx.x];
+        y[row_of[threadIdx.x]] = s;
+    }
+}
+
 // Split-K for short, wide problems (few rows, so too few row workgroups to fill 256 CUs):
 // workgroup b takes row block b / S and K-range b % S of width ks (a multiple of the chunk), so
 // consecutive workgroups still read consecutive memory; the partial sums go to
@@ -479,6 +568,7 @@ struct Variant {
     int threads;         // workgroup size
     gemv_split_fn split = nullptr;  // split-K form (row-per-workgroup variants only)
     int chunk = 0;                  // columns per wave chunk (split width granule)
+    int extra_blocks = 0;           // workgroups past ceil(m / rows): the row-pair forms' last block
 };
 
 #define VEC(LPR, RPG, UNR, NT, OPT)                                                             \
@@ -494,6 +584,9 @@ struct Variant {
      gemv_rowblock_split<NW, RPB, UNR, true>, 128 * UNR}
 #define RWX(NW, RPB, UNR)                                                                  \
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xcd", gemv_rowblock<NW, RPB, UNR, true, 1>, RPB, true, NW * 64}
+#define RWL(NW, UNR, XCD)                                                                  \
+    {"rowlines_w" #NW "_u" #UNR "_x" #XCD, gemv_rowblock_lines<NW, UNR, true, XCD>, 2, true, NW * 64, \
+     nullptr, 0, 16}
 #define RWQ(NW, RPB, UNR, Q)                                                               \
     {"rowblk_w" #NW "_r" #RPB "_u" #UNR "_xq" #Q, gemv_rowblock<NW, RPB, UNR, true, Q>, RPB, true, NW * 64}
 
@@ -564,6 +657,10 @@ static constexpr Variant kVariants[] = {
     VEC(16, 1, 4, 1, 4),           // 63
     VEC(16, 2, 4, 1, 4),           // 64
     VEC(8, 2, 4, 1, 4),            // 65
+    RWL(4, 8, 0),                  // 66 rows off the 128-B lines: line-aligned row pairs
+    RWL(4, 8, 1),                  // 67
+    RWL(8, 4, 0),                  // 68
+    RWL(2, 4, 0),                  // 69
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -589,12 +686,13 @@ constexpr int kVecTwoRows = variant_id(kVariants, "vec_l64_r2_u4_nt1_o7");
 constexpr int kVecFourRows = variant_id(kVariants, "vec_l64_r4_u4_nt1_o5");
 constexpr int kVecOneRow = variant_id(kVariants, "vec_l64_r1_u4_nt1_o5");
 constexpr int kRowLongOdd = variant_id(kVariants, "rowblk_w4_r2_u8_xcd");
+constexpr int kRowLines = variant_id(kVariants, "rowlines_w8_u4_x0");
 constexpr int kVecFourRowsOdd = variant_id(kVariants, "vec_l64_r4_u4_nt1_o0");
 static_assert(kScalarLong > 0 && !kVariants[kScalarLong].vec, "8-B fallback must not need 16-B loads");
 static_assert(kScalarShort > 0 && !kVariants[kScalarShort].vec, "8-B fallback must not need 16-B loads");
 static_assert(kSplitK > 0 && kVariants[kSplitK].split != nullptr, "split-K variant");
 static_assert(kRowLong > 0 && kRowMid > 0 && kRowSmall > 0 && kVecTwoRows > 0 && kVecFourRows > 0 &&
-                  kVecOneRow > 0 && kRowLongOdd > 0 && kVecFourRowsOdd > 0,
+                  kVecOneRow > 0 && kRowLongOdd > 0 && kVecFourRowsOdd > 0 && kRowLines > 0,
               "dispatch names a variant missing from kVariants");
 
 constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4 per CU)
@@ -627,7 +725,12 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 // and per-XCD contiguous streams win there: 16384 x 16383 307 us, 65536 x 8191 609 us, against
 // 329 / 652 for the 8-B kernel); the 2-wave row form for 768 < K < 4096, wave-owns-4-rows for
 // short rows. Only operands off an 8-B boundary keep the 8-B kernels.
-static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool aligned8) {
+// Rows that do not start on 128-B lines (lines == false: an lda not a multiple of 16 or A off
+// a line), long (K >= 6144) and many (M >= 4096): the line-aligned row-pair form
+// (gemv_rowblock_lines; variant_sweep23_lines.jsonl: 16384 x 16386 300 against 313 us,
+// 16384 x 16383 300 / 307, 10200^2 120 / 123, 7800^2 70.5 / 72.1, 65536 x 8191 599 / 609).
+static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool aligned8, bool lines) {
+    if (!lines && aligned8 && K >= 6144 && M >= 4096) return kRowLines;
     const bool vec = aligned && (lda % 2 == 0);
     if (!vec) {
         if (!aligned8) return K >= 256 ? kScalarLong : kScalarShort;
@@ -703,7 +806,10 @@ static int launch(int v, const double* A, int64_t lda, const double* x, double* 
     const int64_t max_rows = max_blocks * var.rows_per_block;
     for (int64_t r0 = 0; r0 < M; r0 += max_rows) {
         const int64_t m = M - r0 < max_rows ? M - r0 : max_rows;
-        const int64_t blocks = (m + var.rows_per_block - 1) / var.rows_per_block;
+        // row-pair forms: a last block of 2p rows with r < 2p rows left needs min(p, r) pairs,
+        // more than ceil(r / 2); up to p = 16 spare workgroups cover it (theirs are rows >= m:
+        // clamped loads, no store)
+        const int64_t blocks = (m + var.rows_per_block - 1) / var.rows_per_block + var.extra_blocks;
         hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(var.threads), 0, s, A + r0 * lda, lda, x,
                            y + r0, m, K);
         MVG_HIP(hipGetLastError());
@@ -1274,7 +1380,9 @@ extern "C" {
 
 int mvg_gemv_variant_count(void) { return kNumVariants; }
 
-int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k) { return pick_variant(lda, m, k, true, true); }
+int mvg_gemv_auto_variant(int64_t lda, int64_t m, int64_t k) {
+    return pick_variant(lda, m, k, true, true, lda % 16 == 0);
+}
 
 const char* mvg_gemv_variant_name(int v) {
     if (v < 0 || v >= kNumVariants) return "invalid";
@@ -1298,7 +1406,8 @@ int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, i
     if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv: lda < k");
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
     const bool aligned8 = ((uintptr_t)A % 8 == 0) && ((uintptr_t)x % 8 == 0);
-    int v = variant == 0 ? pick_variant(lda, m, k, aligned, aligned8) : variant;
+    const bool lines = (uintptr_t)A % 128 == 0 && lda % 16 == 0;  // every row starts on a 128-B line
+    int v = variant == 0 ? pick_variant(lda, m, k, aligned, aligned8, lines) : variant;
     if (kVariants[v].vec && ((uintptr_t)A % 8 != 0 || (uintptr_t)x % 8 != 0))
         return fail(MVG_E_INVALID, "mvg_gemv: 16-B variant needs 8-B aligned A, x");
     return launch(v, A, lda, x, y, m, k, s, variant != 0);

@@ -348,9 +348,13 @@ def test_auto_variant_names_match_the_dispatch_table():
     assert pick(4096, 16384) == "rowblk_w4_r2_u8" and pick(1536, 32768) == "rowblk_w4_r2_u8"
     # below 1 GiB with 768 < K < 8192: row-per-workgroup forms (the reference's test.sh squares)
     assert pick(4200, 4200) == "rowblk_w2_r2_u4" and pick(1800, 1800) == "rowblk_w2_r2_u4"
-    assert pick(7800, 7800) == "rowblk_w8_r2_u4" and pick(1024, 6144) == "rowblk_w2_r2_u4"
+    assert pick(1024, 6144) == "rowblk_w2_r2_u4"
+    # rows off the 128-B lines (lda not a multiple of 16), long and many: line-aligned row pairs
+    assert pick(7800, 7800) == "rowlines_w8_u4_x0" and pick(10200, 10200) == "rowlines_w8_u4_x0"
+    assert pick(16384, 16386) == "rowlines_w8_u4_x0" and pick(16384, 16400) == "rowblk_w4_r2_u8"
     assert names[4096] == "vec_l64_r2_u4_nt1_o7" and names[1024] == "vec_l64_r4_u4_nt1_o5"
     # odd widths (odd lda): the 16-B kernels through unaligned loads, not the 8-B ones
-    assert pick(16384, 16383) == "rowblk_w4_r2_u8_xcd" and pick(65536, 8191) == "rowblk_w4_r2_u8_xcd"
+    assert pick(16384, 16383) == "rowlines_w8_u4_x0" and pick(65536, 8191) == "rowlines_w8_u4_x0"
+    assert pick(2048, 65535) == "rowblk_w4_r2_u8_xcd"
     assert pick(1200, 60001) == "rowblk_w4_r2_u4_splitk" and pick(10200, 1275) == "rowblk_w2_r2_u4"
     assert pick(4200, 525) == "vec_l64_r4_u4_nt1_o0" and pick(524288, 511) == "vec_l64_r4_u4_nt1_o0"
