@@ -77,7 +77,11 @@ def main():
         for v in range(nvar):
             runs[lib.mvg_gemv_exact_variant_name(v).decode()] = (
                 lambda y, v=v: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, v, s))
-        res = {}
+        # calibration: a plain streaming read of A's bytes (every position read once, no chain, no
+        # sliding window) — the rate the exact forms' all-rows-at-once access pattern is held to
+        sink = torch.empty(1 << 20, dtype=torch.float64, device=dev)
+        stream = lambda: lib.mvg_stream_read(A.data_ptr(), M * K, sink.data_ptr(), s)  # noqa: E731
+        res = {"stream_read": {"ms": [], "rel": None, "deterministic": None}}
         y = torch.empty(M, dtype=torch.float64, device=dev)
         for key in list(runs):
             if runs[key](y) != 0:  # a 16-B form refusing an odd lda: not a result
@@ -88,8 +92,9 @@ def main():
             check(fn(y), key)
             res[key] = {"ms": [], "rel": ((y - ref).abs() / ref.abs().clamp_min(1e-300)).max().item(),
                         "deterministic": bool(torch.equal(y, y1))}
+        timed = dict(runs, stream_read=lambda y: stream())
         for _ in range(rounds):
-            for key, fn in runs.items():
+            for key, fn in timed.items():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 check(fn(y), key)
                 e0.record()
