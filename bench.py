@@ -281,11 +281,12 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kms = float(t[0]), float(t[1])
         y = eng.collect()
+        kernel = exact_kernel_name(eng)
     finally:
         eng.set_exact(False)
     out = {"semantics": "mvg_engine_set_exact: y bit-identical to the reference's sequential sums",
            "value": round(total_bytes * steps / el / 1e9, 1), "unit": "GB/s", "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 4), "kernel": exact_kernel_name(eng.shard(0)),
+           "ms_per_step": round(el / steps * 1e3, 4), "kernel": kernel,
            "kernel_ms": round(kms, 5),
            "roofline_frac": round(per_gpu / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None}
     if rank == 0:
@@ -295,9 +296,15 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
     return out, y
 
 
-def exact_kernel_name(sh) -> str:
+def exact_kernel_name(eng) -> str:
+    """The exact kernel shard 0 runs: over its column-panel copy, or the row-major dispatch."""
     from matvec_mpi_multiplier_amd._lib import lib
 
+    sh = eng.shard(0)
+    P = eng.exact_panel_width(0)
+    if P:
+        v = lib.mvg_gemv_exact_panel_auto_variant(sh.n_rows, sh.n_cols)
+        return f"{lib.mvg_gemv_exact_panel_variant_name(v).decode()} (column panels, P = {P})"
     return lib.mvg_gemv_exact_variant_name(lib.mvg_gemv_exact_auto_variant(sh.n_cols, sh.n_rows, sh.n_cols)).decode()
 
 
@@ -372,9 +379,10 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 xsteps = max(5, args.config_steps // 2)
                 xel, xkms = timed(e, xsteps)
                 yx = e.collect()
+                xkernel = exact_kernel_name(e)
                 e.set_exact(False)
                 exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
-                         "steps": xsteps, "kernel": exact_kernel_name(sh), "kernel_ms": round(xkms, 5),
+                         "steps": xsteps, "kernel": xkernel, "kernel_ms": round(xkms, 5),
                          "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
                 if rank == 0:
                     rel = float(np.max(np.abs(yx - y) / np.abs(y)))

@@ -201,6 +201,27 @@ int mvg_gemv_exact_variant_count(void);
 int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k);
 const char* mvg_gemv_exact_variant_name(int variant);
 
+/* The same bit-exact product over A in column panels (the engine's device layout in exact mode,
+ * DESIGN §4b): panel p holds columns [p*P, p*P + P) of all m rows, row i of it at
+ * d_Ap + p*pstride + i*P (pstride >= m*P doubles; the last panel may be narrower than P and is
+ * padded to P). Same sums in the same order as mvg_gemv_exact (multiply_std_rowwise,
+ * src/matr_utils.c:86-96), so y is the same bit for bit; streaming the rows panel by panel reads
+ * one contiguous region at a time instead of m scattered ones. P a power of two, a multiple of
+ * 16 (32 for panel_l16_*); d_Ap and d_x 16-B aligned. variant 0 = auto (names:
+ * mvg_gemv_exact_panel_variant_name, panel_l<L>_w<W>_u<U> as the hop forms). */
+int mvg_gemv_exact_panels(const double* d_Ap, int64_t pstride, int64_t P, const double* d_x, double* d_y,
+                          int64_t m, int64_t k, int variant, void* stream);
+/* Rows [0, m) of a row-major A (lda) into rows [0, m) of the panel layout above (device to
+ * device, HBM-bound; any lda and alignment). Row ranges map onto row ranges: offset d_A by
+ * r0*lda and d_Ap by r0*P, keep pstride. */
+int mvg_panel_relayout(const double* d_A, int64_t lda, int64_t m, int64_t k, double* d_Ap, int64_t pstride,
+                       int64_t P, void* stream);
+/* P the engine uses for an m x k shard in exact mode (0: it keeps the row-major kernels). */
+int64_t mvg_exact_panel_width(int64_t m, int64_t k);
+int mvg_gemv_exact_panel_variant_count(void);
+int mvg_gemv_exact_panel_auto_variant(int64_t m, int64_t k);
+const char* mvg_gemv_exact_panel_variant_name(int variant);
+
 /* Read-only streaming microkernel over `bytes` of device memory (HBM ceiling calibration). */
 int mvg_stream_read(const double* d_src, int64_t n, double* d_sink, void* stream);
 
@@ -264,6 +285,12 @@ int mvg_engine_destroy(mvg_engine* e);
  * result for rank-order message arrival; its own order varies run to run). */
 int mvg_engine_set_exact(mvg_engine* e, int on);
 int mvg_engine_exact(const mvg_engine* e, int* on);
+/* Exact mode keeps a column-panel copy of a tall long-row shard (mvg_exact_panel_width; it must
+ * also fit in free HBM with 8 GiB to spare; MVG_NO_PANELS=1 turns it off) and multiplies it with
+ * mvg_gemv_exact_panels; the copy is rebuilt from the row-major shard by the first multiply after
+ * each distribute / fill and released when exact mode is switched off. *P = the panel width of
+ * local shard i, 0 when it runs the row-major kernels. */
+int mvg_engine_exact_panels(const mvg_engine* e, int local_index, int64_t* P);
 /* Chunked distribution (off by default; MVG_OVERLAP=n in the environment sets it at creation):
  * chunks > 1 makes distribute / distribute_shared move each shard's rows in that many chunks on
  * a copy stream, and the next multiply runs each chunk's GEMV as soon as its rows have landed,

@@ -114,6 +114,12 @@ SIGNATURES = {
     "mvg_gemv_exact_variant_count": (C.c_int, []),
     "mvg_gemv_exact_auto_variant": (C.c_int, [_i64, _i64, _i64]),
     "mvg_gemv_exact_variant_name": (C.c_char_p, [C.c_int]),
+    "mvg_gemv_exact_panels": (C.c_int, [_p, _i64, _i64, _p, _p, _i64, _i64, C.c_int, _p]),
+    "mvg_panel_relayout": (C.c_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p]),
+    "mvg_exact_panel_width": (_i64, [_i64, _i64]),
+    "mvg_gemv_exact_panel_variant_count": (C.c_int, []),
+    "mvg_gemv_exact_panel_auto_variant": (C.c_int, [_i64, _i64]),
+    "mvg_gemv_exact_panel_variant_name": (C.c_char_p, [C.c_int]),
     "mvg_stream_read": (C.c_int, [_p, _i64, _p, _p]),
     "mvg_comm_unique_id": (C.c_int, [C.c_char_p]),
     "mvg_comm_init_all": (C.c_int, [C.POINTER(_p), C.c_int, C.POINTER(C.c_int)]),
@@ -136,6 +142,7 @@ SIGNATURES = {
     "mvg_engine_destroy": (C.c_int, [_p]),
     "mvg_engine_set_exact": (C.c_int, [_p, C.c_int]),
     "mvg_engine_exact": (C.c_int, [_p, C.POINTER(C.c_int)]),
+    "mvg_engine_exact_panels": (C.c_int, [_p, C.c_int, C.POINTER(_i64)]),
     "mvg_engine_set_overlap": (C.c_int, [_p, C.c_int]),
     "mvg_matrix_filename": (C.c_int, [_i64, _i64, C.c_char_p, C.c_size_t]),
     "mvg_vector_filename": (C.c_int, [_i64, C.c_char_p, C.c_size_t]),

@@ -78,6 +78,12 @@ struct Shard {
     hipStream_t xstream = nullptr;      // the exchange step (collectives), overlapping the next GEMV
     double* dA = nullptr;
     double* dx = nullptr;
+    // exact mode, tall long-row shards: the same A in column panels (mvg_gemv_exact_panels),
+    // rebuilt from dA by the second multiply after a write to dA
+    double* dAp = nullptr;
+    int64_t panelP = 0, pstride = 0;
+    bool panels_fresh = false;
+    int64_t uses = 0;  // multiplies since dA was last written
     // local product: y_len (row/block) or R (col) doubles; a ring of kRing buffers when an
     // exchange follows: multiply n writes dy_parts[n % ring] while earlier exchanges still read
     // the others
@@ -122,6 +128,11 @@ struct mvg_engine {
 
 namespace {
 
+bool getenv_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && v[0] == '1';
+}
+
 struct DeviceGuard {
     int prev = 0;
     DeviceGuard() { (void)hipGetDevice(&prev); }
@@ -146,7 +157,7 @@ void free_shard(Shard& s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.copy_stream) (void)hipStreamSynchronize(s.copy_stream);
     if (s.xstream) (void)hipStreamSynchronize(s.xstream);
-    for (double* p : {s.dA, s.dx, s.dy_row, s.dy, s.stage[0], s.stage[1], s.gbuf})
+    for (double* p : {s.dA, s.dAp, s.dx, s.dy_row, s.dy, s.stage[0], s.stage[1], s.gbuf})
         if (p) (void)hipFree(p);
     for (int b = 0; b < kRing; ++b) {
         if (s.dy_parts[b]) (void)hipFree(s.dy_parts[b]);
@@ -529,14 +540,51 @@ int mvg_engine_set_exact(mvg_engine* e, int on) {
     int rc = mvg_engine_sync(e);
     if (rc != MVG_OK) return rc;
     e->exact = on != 0;
-    if (!e->exact || e->alg == MVG_ALG_ROWWISE) return MVG_OK;
     DeviceGuard g;
+    for (auto& s : e->shards) {
+        MVG_HIP(hipSetDevice(s.device));
+        if (!e->exact) {
+            if (s.dAp) (void)hipFree(s.dAp);
+            s.dAp = nullptr;
+            s.panelP = s.pstride = 0;
+            continue;
+        }
+        if (s.dAp || getenv_flag("MVG_NO_PANELS")) continue;
+        // the panel copy only when it pays (mvg_exact_panel_width) and fits beside everything
+        // else with room to spare; otherwise exact mode runs the row-major kernels on dA
+        const mvg_shard& p = s.plan;
+        const int64_t P = mvg_exact_panel_width(p.n_rows, p.n_cols);
+        if (P == 0) continue;
+        const int64_t stride = p.n_rows * P;
+        const int64_t elems = stride * ((p.n_cols + P - 1) / P);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        if ((double)elems * sizeof(double) + (double)(8ll << 30) > (double)free_b) continue;
+        if (hipMalloc((void**)&s.dAp, (size_t)elems * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            s.dAp = nullptr;
+            continue;
+        }
+        s.panelP = P;
+        s.pstride = stride;
+        s.panels_fresh = false;
+    }
+    if (!e->exact || e->alg == MVG_ALG_ROWWISE) return MVG_OK;
     for (auto& s : e->shards) {
         if (s.rank != 0 || s.nsteps == 0 || s.gbuf) continue;
         MVG_HIP(hipSetDevice(s.device));
         const int64_t part = e->alg == MVG_ALG_COLWISE ? e->R : s.plan.y_len;
         if ((rc = alloc_doubles(&s.gbuf, part * e->nranks)) != MVG_OK) return rc;
     }
+    return MVG_OK;
+}
+
+int mvg_engine_exact_panels(const mvg_engine* e, int i, int64_t* P) {
+    if (!e || !P || i < 0 || i >= (int)e->shards.size()) return fail(MVG_E_INVALID, "bad index");
+    *P = e->exact && e->shards[i].dAp ? e->shards[i].panelP : 0;
     return MVG_OK;
 }
 
@@ -571,6 +619,8 @@ int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x) {
     DeviceGuard g;
     int rc;
     for (auto& s : e->shards) {
+        s.panels_fresh = false;
+        s.uses = 0;
         MVG_HIP(hipSetDevice(s.device));
         const mvg_shard& p = s.plan;
         if ((rc = mvg_synth_fill_device(s.dA, p.n_cols, p.n_rows, p.n_cols, p.row_off, p.col_off,
@@ -601,6 +651,7 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
     for (auto& s : e->shards)
         if (s.rank == 0) root = &s;
     if (root && (!x || (!A && e->R * C > 0))) return fail(MVG_E_INVALID, "root needs A and x");
+    for (auto& s : e->shards) s.panels_fresh = false, s.uses = 0;
 
     if (e->single_process) {
         int rc = distribute_direct(e, A, x);
@@ -697,6 +748,7 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
 int mvg_engine_distribute_shared(mvg_engine* e, const double* A, const double* x) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
     if (!x || (!A && e->R * e->C > 0)) return fail(MVG_E_INVALID, "every rank needs the shared A and x");
+    for (auto& s : e->shards) s.panels_fresh = false, s.uses = 0;
     DeviceGuard g;
     int rc = distribute_direct(e, A, x);
     if (rc != MVG_OK) return rc;
@@ -739,6 +791,18 @@ int mvg_engine_multiply(mvg_engine* e) {
         const mvg_shard& p = s.plan;
         if (wait_slot >= 0) MVG_HIP(hipStreamWaitEvent(s.stream, s.x_done[wait_slot], 0));
         double* out = solo ? s.dy : s.dy_parts[b];
+        // exact mode's panel copy of A, rebuilt from dA by the second multiply after a write:
+        // the rebuild moves the shard twice through HBM (about ten multiplies' worth of the
+        // panels' gain), so a distribution that is multiplied once (the reference's timed loop:
+        // distribute + multiply per iteration) never pays for it, and repeated multiplies of
+        // the same A (device-resident) run on panels from the second one on
+        if (e->exact && s.dAp && !s.panels_fresh && s.uses >= 1 && !s.chunks_pending) {
+            int rc = mvg_panel_relayout(s.dA, p.n_cols, p.n_rows, p.n_cols, s.dAp, s.pstride, s.panelP, s.stream);
+            if (rc != MVG_OK) return rc;
+            s.panels_fresh = true;
+        }
+        const bool panels = e->exact && s.dAp && s.panels_fresh;
+        ++s.uses;
         hipEvent_t t0 = nullptr, t1 = nullptr;
         if (timed) {
             if (s.ev_used == s.ev_pool.size()) {
@@ -753,6 +817,9 @@ int mvg_engine_multiply(mvg_engine* e) {
             MVG_HIP(hipEventRecord(t0, s.stream));
         }
         auto gemv = [&](int64_t r0, int64_t rows) {
+            if (panels)
+                return mvg_gemv_exact_panels(s.dAp + r0 * s.panelP, s.pstride, s.panelP, s.dx, out + r0, rows,
+                                             p.n_cols, 0, s.stream);
             return e->exact ? mvg_gemv_exact(s.dA + r0 * p.n_cols, p.n_cols, s.dx, out + r0, rows, p.n_cols, s.stream)
                             : mvg_gemv(s.dA + r0 * p.n_cols, p.n_cols, s.dx, out + r0, rows, p.n_cols, s.stream);
         };

@@ -394,6 +394,94 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
     if (c == holder && row < M) y[row] = sum;
 }
 
+// ------------------------------------------------------------------ column-panel layout
+// Every exact form streams all M rows at once — a row's chain (>= 2.5 ns per column) is too slow
+// for the tree kernel's sliding window of a thousand rows — so at any moment it reads M scattered
+// pieces of a row-major A, one per row: the access pattern of a plain streaming read of
+// thousands of separate ranges, and the same rate (16384^2: exact 312 us, streaming read 309,
+// tree 295; profiles/r02/sweep_exact15_stream_cal.jsonl). With A in column panels — panel p =
+// columns [pP, pP + P) of every row, rows P doubles apart, panels pstride >= M*P doubles apart —
+// the same all-rows-at-once chain order reads one contiguous M*P*8-byte region at a time: a
+// sliding window again, over panels (16384^2: 299 us at P = 256; 65536 x 32768: 2385 against
+// 2466; profiles/r02/panel_probe_*.jsonl). The engine keeps such a copy of its shard in exact
+// mode (engine.cpp). The arithmetic and its order are those of gemv_seq_hop, so y is the same
+// bit for bit. P is a power of two and a multiple of the segment (L*W columns), so no segment
+// straddles two panels; K % (L*W) columns end in one masked segment. Ap 16-B aligned with
+// P*8 a multiple of 128 B puts every segment on a cache line (no head segment).
+template <int L, int W, int U>
+__global__ __launch_bounds__(64) void gemv_seq_hop_panel(const double* __restrict__ Ap, int64_t pstride, int lp,
+                                                         const double* __restrict__ x,
+                                                         double* __restrict__ y, int64_t M, int64_t K) {
+    static_assert(L == 8 || L == 16, "lanes per row");
+    static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B pieces; segment pairs per unrolled step");
+    constexpr int R = 64 / L;  // rows per wave
+    constexpr int S = L * W;   // columns per segment
+    constexpr int V = W / 2;   // 16-B pieces per lane per segment
+    const int lane = threadIdx.x;
+    const int c = lane % L;
+    const int64_t row = (int64_t)blockIdx.x * R + lane / L;
+    const int64_t rr = row < M ? row : M - 1;
+    const int64_t pmask = (1ll << lp) - 1;
+    const double* arow = Ap + (rr << lp);
+    const int off[2] = {c * W, (L - 1 - c) * W};  // even / odd segment
+    // segment g of this row (columns [gS, gS + S)): panel gS >> lp, offset gS & (P - 1) in it
+    auto seg = [&](int64_t g) { return arow + ((g * S) >> lp) * pstride + ((g * S) & pmask); };
+    const int64_t nseg = K / S;
+    const int64_t tail = K - nseg * S;
+    double sum = 0.0;
+    if (nseg > 0) {
+        dbl2x a[U][V], xv[U][V];
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const int64_t g = i < nseg ? i : nseg - 1;
+            load_run<V, false, true>(seg(g) + off[i & 1], a[i]);
+            load_run<V, false, false>(x + g * S + off[i & 1], xv[i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // as in gemv_seq_hop: slot i is summed, then refilled U segments ahead, loads kept in
+        // slot order so the counted vmcnt waits retire exactly the slot about to be summed;
+        // segment g runs forward when g is even (base is a multiple of U, U even)
+        int64_t base = 0;
+        for (; base + U <= nseg; base += U) {
+#pragma unroll
+            for (int i = 0; i < U; ++i) {
+                sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
+                __builtin_amdgcn_sched_barrier(0);
+                const int64_t g = base + i + U < nseg ? base + i + U : nseg - 1;
+                load_run<V, false, true>(seg(g) + off[i & 1], a[i]);
+                load_run<V, false, false>(x + g * S + off[i & 1], xv[i]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            if (base + i < nseg)
+                sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
+    }
+    if (tail > 0) {
+        // the last K % S columns: a masked segment over the panel's columns (zeros outside K);
+        // hop_masked_segment indexes by column, so hand it the segment's base shifted back by gS
+        const int64_t g = nseg;
+        sum = hop_masked_segment<L, W>(sum, seg(g) - g * S, x, g * S + off[g & 1], 0, K, (g & 1) == 0);
+    }
+    const int holder = ((nseg + (tail > 0 ? 1 : 0)) & 1) ? L - 1 : 0;
+    if (c == holder && row < M) y[row] = sum;
+}
+
+// Row-major rows [0, m) of A (lda) -> the same rows of the panel layout (rows P doubles apart,
+// panels pstride apart). One workgroup per row: 64-lane runs of consecutive 8-B elements on both
+// sides (2 KiB per panel row at P = 256), any lda and alignment. HBM-bound: 16 bytes per element.
+__global__ __launch_bounds__(256) void panel_relayout_kernel(const double* __restrict__ A, int64_t lda, int64_t m,
+                                                             int64_t k, double* __restrict__ Ap, int64_t pstride,
+                                                             int lp) {
+    const int64_t pmask = (1ll << lp) - 1;
+    for (int64_t r = blockIdx.x; r < m; r += gridDim.x) {
+        const double* src = A + r * lda;
+        double* dst = Ap + (r << lp);
+        for (int64_t j = threadIdx.x; j < k; j += 256) dst[(j >> lp) * pstride + (j & pmask)] = __builtin_nontemporal_load(src + j);
+    }
+}
+
 // Any alignment, any lda: lane = row, 8-B loads walking the row (uncoalesced; small or odd
 // shapes only).
 __global__ __launch_bounds__(64) void gemv_seq_scalar(const double* __restrict__ A, int64_t lda,
@@ -522,8 +610,8 @@ static bool operands_ok(int needs, int64_t lda, bool aligned) {
     return needs == kVec16 || lda < (1ll << 23);
 }
 
-template <size_t N>
-constexpr int seq_id(const SeqVariant (&table)[N], const char* name) {
+template <typename T, size_t N>
+constexpr int seq_id(const T (&table)[N], const char* name) {
     for (size_t i = 0; i < N; ++i) {
         const char *a = table[i].name, *b = name;
         while (*a && *a == *b) ++a, ++b;
@@ -567,6 +655,34 @@ static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, boo
     if (M >= 2048) return K <= 8192 ? kHopRows : M < 4096 && K >= 32768 ? kHopWidest : kHopWide;
     return K <= 4096 ? kHopWide : kHopFewRows;
 }
+
+// Panel-layout forms (gemv_seq_hop_panel). From profiles/r02/panel_probe_*.jsonl: P = 256
+// (P = 128 within 1 %; 64, 512 and 1024 2-8 % slower, 16 and 4096 well behind), 8 lanes x 16 B
+// per row, 24 segments in flight from 32768 rows (1-2 % ahead there), 8 below (level with 24,
+// 1-3 % ahead of 16).
+typedef void (*panel_fn)(const double*, int64_t, int, const double*, double*, int64_t, int64_t);
+struct PanelVariant {
+    const char* name;
+    panel_fn fn;
+    int rows;  // rows per one-wave workgroup
+    int seg;   // columns per segment (P must be a multiple)
+};
+#define PANEL(L, W, U) {"panel_l" #L "_w" #W "_u" #U, gemv_seq_hop_panel<L, W, U>, 64 / L, L * W}
+static constexpr PanelVariant kPanelVariants[] = {
+    {"auto", nullptr, 8, 16},  // 0
+    PANEL(8, 2, 8),
+    PANEL(8, 2, 16),
+    PANEL(8, 2, 24),
+    PANEL(16, 2, 16),
+};
+#undef PANEL
+constexpr int kNumPanelVariants = (int)(sizeof(kPanelVariants) / sizeof(kPanelVariants[0]));
+constexpr int kPanelRows = seq_id(kPanelVariants, "panel_l8_w2_u8");
+constexpr int kPanelLongRows = seq_id(kPanelVariants, "panel_l8_w2_u24");
+static_assert(kPanelRows > 0 && kPanelLongRows > 0, "panel dispatch names a missing variant");
+constexpr int64_t kPanelWidth = 256;
+
+static int pick_panel_variant(int64_t M) { return M >= 32768 ? kPanelLongRows : kPanelRows; }
 
 }  // namespace mvg
 
@@ -620,6 +736,76 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
 int mvg_gemv_exact(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
                    void* stream) {
     return mvg_gemv_exact_variant(A, lda, x, y, m, k, 0, stream);
+}
+
+// ---- column-panel layout (gemv_seq_hop_panel; the engine's exact mode)
+int64_t mvg_exact_panel_width(int64_t m, int64_t k) {
+    // where the panels beat the row-major exact dispatch (profiles/r02/panel_probe_product*.jsonl,
+    // 15 shapes, and the bench's configs): the 8-lane hop forms' domain (>= 6144 rows), at least
+    // 8 panels and 128 MiB (6144 x 2048 ran 4 % slower on panels), not the few-row long-row
+    // corner (8192 x 16384: 3 % slower; its 1024 waves are one per SIMD), and at most 16 GiB:
+    // 65536^2 (32 GiB) was 1.5 % faster on one box and 2 % slower on another, 131072^2 (128 GiB,
+    // config 4 on one GPU) 3 % slower; in between 1.3-18 % faster
+    if (m < 6144 || k < 2048 || m * k < (1ll << 24) || m * k > (1ll << 31)) return 0;
+    if (m <= 8192 && k > 8192) return 0;
+    return kPanelWidth;
+}
+
+int mvg_gemv_exact_panel_variant_count(void) { return kNumPanelVariants; }
+
+const char* mvg_gemv_exact_panel_variant_name(int v) {
+    if (v < 0 || v >= kNumPanelVariants) return "invalid";
+    return kPanelVariants[v].name;
+}
+
+int mvg_gemv_exact_panel_auto_variant(int64_t m, int64_t k) {
+    (void)k;
+    return pick_panel_variant(m);
+}
+
+static int panel_log2(int64_t P) {
+    int lp = 0;
+    while ((1ll << lp) < P) ++lp;
+    return (1ll << lp) == P ? lp : -1;
+}
+
+int mvg_panel_relayout(const double* A, int64_t lda, int64_t m, int64_t k, double* Ap, int64_t pstride, int64_t P,
+                       void* stream) {
+    const int lp = P > 0 ? panel_log2(P) : -1;
+    if (m < 0 || k < 0 || lp < 0 || lda < k) return fail(MVG_E_INVALID, "mvg_panel_relayout: bad shape or panel width");
+    if (m == 0 || k == 0) return MVG_OK;
+    if (!A || !Ap) return fail(MVG_E_INVALID, "mvg_panel_relayout: null pointer");
+    if (pstride < m * P && (k + P - 1) / P > 1) return fail(MVG_E_INVALID, "mvg_panel_relayout: pstride < m * P");
+    const int64_t blocks = m < (1ll << 20) ? m : (1ll << 20);
+    hipLaunchKernelGGL(panel_relayout_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A, lda, m, k,
+                       Ap, pstride, lp);
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
+}
+
+int mvg_gemv_exact_panels(const double* Ap, int64_t pstride, int64_t P, const double* x, double* y, int64_t m,
+                          int64_t k, int variant, void* stream) {
+    if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: negative size");
+    if (variant < 0 || variant >= kNumPanelVariants) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: bad variant");
+    if (m == 0) return MVG_OK;
+    if (!y) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: null y");
+    const int v = variant == 0 ? pick_panel_variant(m) : variant;
+    const int lp = P > 0 ? panel_log2(P) : -1;
+    if (lp < 0 || P % kPanelVariants[v].seg != 0)
+        return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: P must be a power of two and a multiple of the segment");
+    if (k > 0) {
+        if (!Ap || !x) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: null A or x");
+        if ((uintptr_t)Ap % 16 || (uintptr_t)x % 16)
+            return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: A and x must be 16-B aligned");
+        if (pstride < m * P && (k + P - 1) / P > 1) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: pstride < m * P");
+    }
+    const int rw = kPanelVariants[v].rows;
+    const int64_t blocks = (m + rw - 1) / rw;
+    if (blocks >= (1ll << 31)) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: too many rows for one launch");
+    hipLaunchKernelGGL(kPanelVariants[v].fn, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, Ap, pstride, lp,
+                       x, y, m, k);
+    MVG_HIP(hipGetLastError());
+    return MVG_OK;
 }
 
 }  // extern "C"

@@ -341,6 +341,12 @@ class Multiplier:
         check(lib.mvg_engine_exact(self.handle, C.byref(v)), "mvg_engine_exact")
         return bool(v.value)
 
+    def exact_panel_width(self, i: int = 0) -> int:
+        """Panel width of local shard i's column-panel copy in exact mode (0: row-major kernels)."""
+        v = C.c_int64()
+        check(lib.mvg_engine_exact_panels(self.handle, i, C.byref(v)), "mvg_engine_exact_panels")
+        return v.value
+
     def kernel_timing(self, every: int) -> None:
         """Bracket every `every`-th multiply's GEMV with HIP events (0 = off)."""
         check(lib.mvg_engine_kernel_timing(self.handle, int(every)), "mvg_engine_kernel_timing")

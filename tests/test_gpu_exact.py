@@ -262,3 +262,141 @@ def test_multiply_std_rowwise_host_entry_point():
     _lib.check(lib.mvg_multiply_std_rowwise(None, None, 0, 0, None, 0), "release")
     with pytest.raises(_lib.MvgError):
         _lib.check(lib.mvg_multiply_std_rowwise(None, None, 3, 3, None, 1), "null")
+
+
+# ---------------------------------------------------------------- column-panel layout
+def panel_variants():
+    lib = _lib.lib
+    return [(v, lib.mvg_gemv_exact_panel_variant_name(v).decode())
+            for v in range(lib.mvg_gemv_exact_panel_variant_count())]
+
+
+def panels_of(A, P):
+    """Host restatement of the panel layout (mvg_panel_relayout): panel p = columns
+    [pP, pP + P) of every row, rows P apart, panels m*P apart, the last one padded to P."""
+    m, k = A.shape
+    npan = -(-k // P)
+    out = np.zeros((npan, m, P))
+    for p in range(npan):
+        w = min(P, k - p * P)
+        out[p, :, :w] = A[:, p * P:p * P + w]
+    return out
+
+
+@pytest.mark.parametrize("m,k", [(1, 16), (9, 2048), (65, 4096 + 2), (130, 257), (1000, 1536), (61, 16388),
+                                 (640, 8191), (3, 1), (8, 0)])
+def test_gemv_exact_panels_every_variant_is_the_reference_sum(m, k):
+    # the relayout kernel against the host restatement of the layout, then every panel variant
+    # and panel width over it against the oracle, bit for bit (mixed signs; column tails of every
+    # length; rows past the last whole wave; a padded row-major source with lda > k)
+    lib = _lib.lib
+    lda = k + 3
+    A = signed(oracle.synth(m, lda, 42), m + k)
+    x = signed(oracle.synth(1, k, 4242)[0], k + 1) if k else np.zeros(1)
+    want = oracle.multiply_std_rowwise(np.ascontiguousarray(A[:, :k]), x[:k])
+    dA, dx, dy = mm.DeviceBuffer(m * lda).upload(A), mm.DeviceBuffer(max(k, 1)).upload(x), mm.DeviceBuffer(m)
+    for P in (16, 32, 256):
+        npan = max(-(-k // P), 1)
+        dAp = mm.DeviceBuffer(npan * m * P).upload(np.zeros(npan * m * P))
+        _lib.check(lib.mvg_panel_relayout(dA.ptr, lda, m, k, dAp.ptr, m * P, P, None), "relayout")
+        _lib.check(lib.mvg_stream_sync(None), "sync")
+        if k:
+            assert np.array_equal(dAp.download().reshape(npan, m, P), panels_of(A[:, :k], P)), P
+        for v, name in panel_variants():
+            seg = 32 if name.startswith("panel_l16") else 16
+            rc = lib.mvg_gemv_exact_panels(dAp.ptr, m * P, P, dx.ptr, dy.ptr, m, k, v, None)
+            if P % seg:
+                assert rc != 0, (name, P)
+                continue
+            _lib.check(rc, name)
+            _lib.check(lib.mvg_stream_sync(None), "sync")
+            assert np.array_equal(dy.download(), want), (name, P, m, k)
+        dAp.free()
+
+
+def test_gemv_exact_panels_row_ranges_and_refusals():
+    # the engine's chunked distribution relays out and multiplies row ranges (d_A + r0*lda,
+    # d_Ap + r0*P, the whole shard's pstride): the pieces must give the whole y
+    lib = _lib.lib
+    m, k, P = 3001, 5000, 256
+    A = signed(oracle.synth(m, k, 42), 3)
+    x = signed(oracle.synth(1, k, 4242)[0], 4)
+    want = oracle.multiply_std_rowwise(A, x)
+    npan = -(-k // P)
+    dA, dx, dy = mm.DeviceBuffer(m * k).upload(A), mm.DeviceBuffer(k).upload(x), mm.DeviceBuffer(m)
+    dAp = mm.DeviceBuffer(npan * m * P)
+    for r0, r1 in [(0, 1000), (1000, 1001), (1001, 2999), (2999, 3001)]:
+        _lib.check(lib.mvg_panel_relayout(dA.ptr + 8 * r0 * k, k, r1 - r0, k, dAp.ptr + 8 * r0 * P, m * P, P, None), "rl")
+        _lib.check(lib.mvg_gemv_exact_panels(dAp.ptr + 8 * r0 * P, m * P, P, dx.ptr, dy.ptr + 8 * r0, r1 - r0, k, 0,
+                                             None), "gemv")
+    _lib.check(lib.mvg_stream_sync(None), "sync")
+    assert np.array_equal(dy.download(), want)
+    assert lib.mvg_gemv_exact_panels(dAp.ptr, m * P, 96, dx.ptr, dy.ptr, m, k, 0, None) != 0  # P not 2^n
+    assert lib.mvg_gemv_exact_panels(dAp.ptr, m * P, P, dx.ptr + 8, dy.ptr, m, k, 0, None) != 0  # x off 16 B
+    assert lib.mvg_gemv_exact_panels(dAp.ptr, m * P - 1, P, dx.ptr, dy.ptr, m, k, 0, None) != 0  # pstride
+    assert lib.mvg_panel_relayout(dA.ptr, k - 1, m, k, dAp.ptr, m * P, P, None) != 0  # lda < k
+
+
+@pytest.mark.parametrize("alg", ["rowwise", "colwise"])
+@pytest.mark.parametrize("overlap", [0, 3])
+def test_engine_exact_panels_equal_row_major_exact(alg, overlap, monkeypatch):
+    # a shard the engine keeps in panels in exact mode (>= 6144 rows, >= 2048 columns, a column
+    # tail): y identical to the row-major exact kernels (MVG_NO_PANELS=1) and to the oracle,
+    # across a redistribution with new values (the panel copy must be rebuilt), with the
+    # distribution whole or in row chunks behind which the GEMVs run. The first multiply after
+    # a distribution runs the row-major kernels, the second builds the panel copy and runs on
+    # it: both ys are checked.
+    R, Cn = 6160, 4098
+    assert _lib.lib.mvg_exact_panel_width(R, Cn) > 0
+    A1, x1 = signed(oracle.synth(R, Cn, 42), 1), signed(oracle.synth(1, Cn, 4242)[0], 2)
+    A2, x2 = signed(oracle.synth(R, Cn, 43), 3), signed(oracle.synth(1, Cn, 4243)[0], 4)
+    ys = {}
+    for no_panels in ("0", "1"):
+        monkeypatch.setenv("MVG_NO_PANELS", no_panels)
+        c = mm.Comm.init_all([0])
+        try:
+            with mm.Multiplier(alg, R, Cn, c, exact=True) as e:
+                e.set_overlap(overlap)
+                out = []
+                assert (e.exact_panel_width() > 0) == (no_panels == "0")
+                for A, x in ((A1, x1), (A2, x2)):
+                    e.distribute(A, x)
+                    e.multiply()
+                    out.append(e.collect())
+                    e.multiply()
+                    out.append(e.collect())
+                ys[no_panels] = out
+        finally:
+            c.destroy()
+    for i, (A, x) in enumerate(((A1, x1), (A1, x1), (A2, x2), (A2, x2))):
+        want = oracle.multiply_std_rowwise(A, x)
+        assert np.array_equal(ys["1"][i], want), (alg, i)
+        assert np.array_equal(ys["0"][i], want), (alg, i)
+
+
+def test_engine_exact_panels_fill_synth_and_toggle(comm1):
+    # device-resident inputs: exact on (row-major first, then panels built by the second
+    # multiply), off (tree kernel on dA, panel copy released), on again (rebuilt at once: dA has
+    # been multiplied since the fill) — sampled rows against the oracle bit for bit
+    R, Cn = 8192, 4096
+    with mm.Multiplier("rowwise", R, Cn, comm1) as e:
+        e.fill_synth()
+        e.set_exact(True)
+        assert e.exact_panel_width() == 256
+        e.multiply()
+        y0 = e.collect()
+        e.multiply()
+        y1 = e.collect()
+        e.set_exact(False)
+        assert e.exact_panel_width() == 0
+        e.multiply()
+        yt = e.collect()
+        e.set_exact(True)
+        e.multiply()
+        y2 = e.collect()
+    assert np.array_equal(y0, y1) and np.array_equal(y1, y2)
+    assert max_rel(yt, y1) <= 1e-12
+    x = oracle.synth(1, Cn, mm.SEED_X)[0]
+    for r in [0, 1, 7, 8, R // 2, R - 1]:
+        Ar = oracle.synth_block(r, 1, 0, Cn, Cn, mm.SEED_A)
+        assert oracle.multiply_std_rowwise(Ar, x)[0] == y1[r], r
