@@ -1,7 +1,11 @@
 """Launch the bit-exact GEMV (and, for comparison, the tree-summed one) on one device-resident
 shape, for rocprofv3 counter passes (development tool).
 
-    python tools/exact_probe.py [M] [K] [launches] [exact variant name or "auto"]
+    python tools/exact_probe.py [M] [K] [launches] [exact variant name, "auto" or "panels"]
+
+"panels": the shard is rewritten once into the engine's column-panel layout
+(mvg_panel_relayout, P = mvg_exact_panel_width or 256) and the exact launches run
+mvg_gemv_exact_panels on it.
 """
 import os
 import sys
@@ -17,14 +21,20 @@ def main():
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     name = sys.argv[4] if len(sys.argv) > 4 else "auto"
     v = 0
-    if name != "auto":
+    if name not in ("auto", "panels"):
         names = [lib.mvg_gemv_exact_variant_name(i).decode() for i in range(lib.mvg_gemv_exact_variant_count())]
         v = names.index(name)
     dA, dx, dy = mm.DeviceBuffer(M * K), mm.DeviceBuffer(K), mm.DeviceBuffer(M)
     check(lib.mvg_synth_fill_device(dA.ptr, K, M, K, 0, 0, K, 42, None), "fill A")
     check(lib.mvg_synth_fill_device(dx.ptr, K, 1, K, 0, 0, K, 4242, None), "fill x")
+    exact = lambda: lib.mvg_gemv_exact_variant(dA.ptr, K, dx.ptr, dy.ptr, M, K, v, None)  # noqa: E731
+    if name == "panels":
+        P = lib.mvg_exact_panel_width(M, K) or 256
+        dAp = mm.DeviceBuffer(M * P * (-(-K // P)))
+        check(lib.mvg_panel_relayout(dA.ptr, K, M, K, dAp.ptr, M * P, P, None), "relayout")
+        exact = lambda: lib.mvg_gemv_exact_panels(dAp.ptr, M * P, P, dx.ptr, dy.ptr, M, K, 0, None)  # noqa: E731
     for _ in range(n):
-        check(lib.mvg_gemv_exact_variant(dA.ptr, K, dx.ptr, dy.ptr, M, K, v, None), "exact")
+        check(exact(), "exact")
         check(lib.mvg_gemv(dA.ptr, K, dx.ptr, dy.ptr, M, K, None), "tree")
     check(lib.mvg_stream_sync(None), "sync")
     print(f"exact_probe {M}x{K}: {n} launches of {name} and of the tree kernel")
