@@ -212,6 +212,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "gflops": round(2 * R * C * args.steps / elapsed / 1e9, 1),  # whole job, 2 flops per element of A
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -286,7 +287,8 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
         eng.set_exact(False)
     out = {"semantics": "mvg_engine_set_exact: y bit-identical to the reference's sequential sums",
            "value": round(total_bytes * steps / el / 1e9, 1), "unit": "GB/s", "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 4), "kernel": kernel,
+           "ms_per_step": round(el / steps * 1e3, 4), "gflops": round(2 * eng.R * eng.C * steps / el / 1e9, 1),
+           "kernel": kernel,
            "kernel_ms": round(kms, 5),
            "roofline_frac": round(per_gpu / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None}
     if rank == 0:
@@ -382,6 +384,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 xkernel = exact_kernel_name(e)
                 e.set_exact(False)
                 exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
+                         "gflops": round(2 * R * C * xsteps / xel / 1e9, 1),
                          "steps": xsteps, "kernel": xkernel, "kernel_ms": round(xkms, 5),
                          "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
                 if rank == 0:
@@ -396,6 +399,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             "grid": [gr, gc] if alg == "blockwise" else None,
             "value": round(total * args.config_steps / el / 1e9, 1), "unit": "GB/s",
             "ms_per_step": round(el / args.config_steps * 1e3, 4), "steps": args.config_steps,
+            "gflops": round(2 * R * C * args.config_steps / el / 1e9, 1),
             "kernel": kernel_name(sh), "kernel_ms": round(kms, 5),
             "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
             "exact": exact,
@@ -431,7 +435,8 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
         if rank == 0:
             assert np.array_equal(y, y_ref), "end-to-end y differs from the device-resident y"
         return {"mean_s": float(np.mean(times)), "iters": len(times),
-                "GBps": total_bytes / float(np.mean(times)) / 1e9}
+                "GBps": total_bytes / float(np.mean(times)) / 1e9,
+                "gflops": 2 * R * C / float(np.mean(times)) / 1e9}
 
     out = {"semantics": "reference: root holds A, x in host memory; distribute + multiply + y on root"}
     from matvec_mpi_multiplier_amd.hostshare import SharedHostMatrix, shm_free_bytes
