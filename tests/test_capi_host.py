@@ -366,3 +366,43 @@ def test_auto_variant_names_match_the_dispatch_table():
     assert pick(2048, 65535) == "rowblk_w4_r2_u8_xcd"
     assert pick(1200, 60001) == "rowblk_w4_r2_u4_splitk" and pick(10200, 1275) == "rowblk_w2_r2_u4"
     assert pick(4200, 525) == "vec_l64_r4_u4_nt1_o0" and pick(524288, 511) == "vec_l64_r4_u4_nt1_o0"
+
+
+def test_exact_panel_dispatch_and_argument_checks():
+    # host-only parts of the column-panel exact path: where the engine keeps a
+    # panel copy, which variant runs it, and the argument checks that refuse before any launch
+    lib = _lib.lib
+    width = lib.mvg_exact_panel_width
+    assert width(16384, 16384) == 256            # config 2
+    assert width(65536, 32768) == 256            # config 4's block at G = 8 (16 GiB)
+    assert width(65536, 8192) == 256             # config 3's strip at G = 8
+    assert width(10200, 10200) == 256 and width(7800, 7800) == 256  # the reference's sizes
+    assert width(65536, 65536) == 0              # above 16 GiB: row-major forms
+    assert width(131072, 131072) == 0
+    assert width(8192, 16384) == 0               # few rows, long rows
+    assert width(6144, 2048) == 0                # under 128 MiB
+    assert width(4096, 65536) == 0 and width(4194304, 512) == 0  # few rows / short rows
+    name = lambda m, k: lib.mvg_gemv_exact_panel_variant_name(lib.mvg_gemv_exact_panel_auto_variant(m, k)).decode()  # noqa: E731
+    assert name(16384, 16384) == "panel_l8_w2_u8" and name(65536, 8192) == "panel_l8_w2_u24"
+    names = [lib.mvg_gemv_exact_panel_variant_name(v).decode() for v in range(lib.mvg_gemv_exact_panel_variant_count())]
+    assert names[0] == "auto" and all(n.startswith("panel_l") for n in names[1:])
+    assert lib.mvg_gemv_exact_panel_variant_name(len(names)) == b"invalid"
+    fake = 1 << 20  # never dereferenced: every call below is refused before a launch
+    bad = [
+        lib.mvg_gemv_exact_panels(fake, 256 * 64, 96, fake, fake, 64, 1000, 0, None),       # P not a power of 2
+        lib.mvg_gemv_exact_panels(fake, 256 * 64, 8, fake, fake, 64, 1000, 0, None),        # P < segment
+        lib.mvg_gemv_exact_panels(fake, 256 * 64 - 1, 256, fake, fake, 64, 1000, 0, None),  # pstride < m*P
+        lib.mvg_gemv_exact_panels(fake + 8, 256 * 64, 256, fake, fake, 64, 1000, 0, None),  # A off 16 B
+        lib.mvg_gemv_exact_panels(fake, 256 * 64, 256, fake + 8, fake, 64, 1000, 0, None),  # x off 16 B
+        lib.mvg_gemv_exact_panels(fake, 256 * 64, 256, fake, fake, -1, 1000, 0, None),      # negative m
+        lib.mvg_gemv_exact_panels(fake, 256 * 64, 256, fake, fake, 64, 1000, len(names), None),  # variant
+        lib.mvg_gemv_exact_panels(None, 256 * 64, 256, None, fake, 64, 1000, 0, None),      # null A, x
+        lib.mvg_panel_relayout(fake, 999, 64, 1000, fake, 256 * 64, 256, None),             # lda < k
+        lib.mvg_panel_relayout(fake, 1000, 64, 1000, fake, 256 * 64, 100, None),            # P not 2^n
+        lib.mvg_panel_relayout(fake, 1000, 64, 1000, fake, 256 * 63, 256, None),            # pstride
+        lib.mvg_panel_relayout(None, 1000, 64, 1000, fake, 256 * 64, 256, None),            # null
+    ]
+    assert all(rc == _lib.MVG_E_INVALID for rc in bad), bad
+    # nothing to do is not an error (no launch either)
+    assert lib.mvg_gemv_exact_panels(None, 0, 256, None, None, 0, 1000, 0, None) == 0
+    assert lib.mvg_panel_relayout(None, 0, 0, 0, None, 0, 256, None) == 0
