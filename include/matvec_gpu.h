@@ -285,11 +285,12 @@ int mvg_engine_destroy(mvg_engine* e);
  * result for rank-order message arrival; its own order varies run to run). */
 int mvg_engine_set_exact(mvg_engine* e, int on);
 int mvg_engine_exact(const mvg_engine* e, int* on);
-/* Exact mode keeps a column-panel copy of a tall long-row shard (mvg_exact_panel_width; it must
- * also fit in free HBM with 8 GiB to spare; MVG_NO_PANELS=1 turns it off) and multiplies it with
- * mvg_gemv_exact_panels; the copy is rebuilt from the row-major shard by the first multiply after
- * each distribute / fill and released when exact mode is switched off. *P = the panel width of
- * local shard i, 0 when it runs the row-major kernels. */
+/* Exact mode keeps a column-panel copy of a tall long-row shard (mvg_exact_panel_width) and
+ * multiplies it with mvg_gemv_exact_panels: the copy is allocated (if it fits in free HBM with
+ * 8 GiB to spare) and rebuilt from the row-major shard by the second multiply after each
+ * distribute / fill — a distribution multiplied once never pays for it — and released when exact
+ * mode is switched off; MVG_NO_PANELS=1 turns it off. *P = the panel width of local shard i's
+ * copy, 0 while it runs the row-major kernels. */
 int mvg_engine_exact_panels(const mvg_engine* e, int local_index, int64_t* P);
 /* Chunked distribution (off by default; MVG_OVERLAP=n in the environment sets it at creation):
  * chunks > 1 makes distribute / distribute_shared move each shard's rows in that many chunks on

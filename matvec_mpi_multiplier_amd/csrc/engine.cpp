@@ -79,7 +79,7 @@ struct Shard {
     double* dA = nullptr;
     double* dx = nullptr;
     // exact mode, tall long-row shards: the same A in column panels (mvg_gemv_exact_panels),
-    // rebuilt from dA by the second multiply after a write to dA
+    // allocated and rebuilt from dA by the second multiply after a write to dA
     double* dAp = nullptr;
     int64_t panelP = 0, pstride = 0;
     bool panels_fresh = false;
@@ -127,6 +127,21 @@ struct mvg_engine {
 };
 
 namespace {
+
+// Exact mode's column-panel copy of a shard (s.panelP > 0), allocated when first needed if it
+// fits in free HBM with 8 GiB to spare; otherwise the shard keeps the row-major exact kernels
+// (panelP = 0 until exact mode is switched on again).
+void alloc_panels(Shard& s) {
+    const int64_t elems = s.pstride * ((s.plan.n_cols + s.panelP - 1) / s.panelP);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
+        (double)elems * sizeof(double) + (double)(8ll << 30) > (double)free_b ||
+        hipMalloc((void**)&s.dAp, (size_t)elems * sizeof(double)) != hipSuccess) {
+        (void)hipGetLastError();
+        s.dAp = nullptr;
+        s.panelP = s.pstride = 0;
+    }
+}
 
 bool getenv_flag(const char* name) {
     const char* v = getenv(name);
@@ -550,26 +565,10 @@ int mvg_engine_set_exact(mvg_engine* e, int on) {
             continue;
         }
         if (s.dAp || getenv_flag("MVG_NO_PANELS")) continue;
-        // the panel copy only when it pays (mvg_exact_panel_width) and fits beside everything
-        // else with room to spare; otherwise exact mode runs the row-major kernels on dA
-        const mvg_shard& p = s.plan;
-        const int64_t P = mvg_exact_panel_width(p.n_rows, p.n_cols);
-        if (P == 0) continue;
-        const int64_t stride = p.n_rows * P;
-        const int64_t elems = stride * ((p.n_cols + P - 1) / P);
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-            (void)hipGetLastError();
-            continue;
-        }
-        if ((double)elems * sizeof(double) + (double)(8ll << 30) > (double)free_b) continue;
-        if (hipMalloc((void**)&s.dAp, (size_t)elems * sizeof(double)) != hipSuccess) {
-            (void)hipGetLastError();
-            s.dAp = nullptr;
-            continue;
-        }
-        s.panelP = P;
-        s.pstride = stride;
+        // the panel copy where it pays (mvg_exact_panel_width); allocated by the multiply that
+        // first needs it (alloc_panels), so a distribute-per-multiply loop never holds one
+        s.panelP = mvg_exact_panel_width(s.plan.n_rows, s.plan.n_cols);
+        s.pstride = s.plan.n_rows * s.panelP;
         s.panels_fresh = false;
     }
     if (!e->exact || e->alg == MVG_ALG_ROWWISE) return MVG_OK;
@@ -796,10 +795,13 @@ int mvg_engine_multiply(mvg_engine* e) {
         // panels' gain), so a distribution that is multiplied once (the reference's timed loop:
         // distribute + multiply per iteration) never pays for it, and repeated multiplies of
         // the same A (device-resident) run on panels from the second one on
-        if (e->exact && s.dAp && !s.panels_fresh && s.uses >= 1 && !s.chunks_pending) {
-            int rc = mvg_panel_relayout(s.dA, p.n_cols, p.n_rows, p.n_cols, s.dAp, s.pstride, s.panelP, s.stream);
-            if (rc != MVG_OK) return rc;
-            s.panels_fresh = true;
+        if (e->exact && s.panelP && !s.panels_fresh && s.uses >= 1 && !s.chunks_pending) {
+            if (!s.dAp) alloc_panels(s);
+            if (s.dAp) {
+                int rc = mvg_panel_relayout(s.dA, p.n_cols, p.n_rows, p.n_cols, s.dAp, s.pstride, s.panelP, s.stream);
+                if (rc != MVG_OK) return rc;
+                s.panels_fresh = true;
+            }
         }
         const bool panels = e->exact && s.dAp && s.panels_fresh;
         ++s.uses;

@@ -358,13 +358,14 @@ def test_engine_exact_panels_equal_row_major_exact(alg, overlap, monkeypatch):
             with mm.Multiplier(alg, R, Cn, c, exact=True) as e:
                 e.set_overlap(overlap)
                 out = []
-                assert (e.exact_panel_width() > 0) == (no_panels == "0")
                 for A, x in ((A1, x1), (A2, x2)):
                     e.distribute(A, x)
                     e.multiply()
                     out.append(e.collect())
+                    assert e.exact_panel_width() == 0 or A is A2  # allocated by the 2nd multiply
                     e.multiply()
                     out.append(e.collect())
+                    assert (e.exact_panel_width() > 0) == (no_panels == "0")
                 ys[no_panels] = out
         finally:
             c.destroy()
@@ -382,11 +383,12 @@ def test_engine_exact_panels_fill_synth_and_toggle(comm1):
     with mm.Multiplier("rowwise", R, Cn, comm1) as e:
         e.fill_synth()
         e.set_exact(True)
-        assert e.exact_panel_width() == 256
         e.multiply()
         y0 = e.collect()
+        assert e.exact_panel_width() == 0  # a fill multiplied once: no panel copy yet
         e.multiply()
         y1 = e.collect()
+        assert e.exact_panel_width() == 256
         e.set_exact(False)
         assert e.exact_panel_width() == 0
         e.multiply()
