@@ -40,6 +40,11 @@ SHAPES = {
     "mid_6144x4096": (6144, 4096),
     "tall_262144x4096": (262144, 4096),
     "tall_1048576x2048": (1048576, 2048),
+    "ref_4200sq": (4200, 4200),
+    "ref_5400sq": (5400, 5400),
+    "mid_4096x16384": (4096, 16384),
+    "mid_4096x32768": (4096, 32768),
+    "mid_2048x65536": (2048, 65536),
 }
 
 
