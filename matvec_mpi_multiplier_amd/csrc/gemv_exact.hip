@@ -469,8 +469,11 @@ __global__ __launch_bounds__(64) void gemv_seq_hop_panel(const double* __restric
 }
 
 // Row-major rows [0, m) of A (lda) -> the same rows of the panel layout (rows P doubles apart,
-// panels pstride apart). One workgroup per row: 64-lane runs of consecutive 8-B elements on both
-// sides (2 KiB per panel row at P = 256), any lda and alignment. HBM-bound: 16 bytes per element.
+// panels pstride apart). One workgroup per row: 64-lane runs of consecutive elements on both
+// sides (2 KiB per panel row at P = 256). V16: 16-B pairs (A 16-B aligned, lda even; P, pstride
+// and the pair's column even, so a pair never straddles two panels and lands 16-B aligned),
+// else 8-B elements (any lda and alignment). HBM-bound: 16 bytes moved per element.
+template <bool V16>
 __global__ __launch_bounds__(256) void panel_relayout_kernel(const double* __restrict__ A, int64_t lda, int64_t m,
                                                              int64_t k, double* __restrict__ Ap, int64_t pstride,
                                                              int lp) {
@@ -478,7 +481,17 @@ __global__ __launch_bounds__(256) void panel_relayout_kernel(const double* __res
     for (int64_t r = blockIdx.x; r < m; r += gridDim.x) {
         const double* src = A + r * lda;
         double* dst = Ap + (r << lp);
-        for (int64_t j = threadIdx.x; j < k; j += 256) dst[(j >> lp) * pstride + (j & pmask)] = __builtin_nontemporal_load(src + j);
+        if constexpr (V16) {
+            const dbl2x* src2 = reinterpret_cast<const dbl2x*>(src);
+            for (int64_t q = threadIdx.x; q < k / 2; q += 256) {
+                const int64_t j = 2 * q;
+                *reinterpret_cast<dbl2x*>(dst + (j >> lp) * pstride + (j & pmask)) = __builtin_nontemporal_load(src2 + q);
+            }
+            if ((k & 1) && threadIdx.x == 0) dst[((k - 1) >> lp) * pstride + ((k - 1) & pmask)] = src[k - 1];
+        } else {
+            for (int64_t j = threadIdx.x; j < k; j += 256)
+                dst[(j >> lp) * pstride + (j & pmask)] = __builtin_nontemporal_load(src + j);
+        }
     }
 }
 
@@ -777,8 +790,13 @@ int mvg_panel_relayout(const double* A, int64_t lda, int64_t m, int64_t k, doubl
     if (!A || !Ap) return fail(MVG_E_INVALID, "mvg_panel_relayout: null pointer");
     if (pstride < m * P && (k + P - 1) / P > 1) return fail(MVG_E_INVALID, "mvg_panel_relayout: pstride < m * P");
     const int64_t blocks = m < (1ll << 20) ? m : (1ll << 20);
-    hipLaunchKernelGGL(panel_relayout_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A, lda, m, k,
-                       Ap, pstride, lp);
+    const bool v16 = (uintptr_t)A % 16 == 0 && (uintptr_t)Ap % 16 == 0 && lda % 2 == 0 && P % 2 == 0 && pstride % 2 == 0;
+    if (v16)
+        hipLaunchKernelGGL(panel_relayout_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A,
+                           lda, m, k, Ap, pstride, lp);
+    else
+        hipLaunchKernelGGL(panel_relayout_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A,
+                           lda, m, k, Ap, pstride, lp);
     MVG_HIP(hipGetLastError());
     return MVG_OK;
 }
