@@ -278,7 +278,8 @@ int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches);
 int mvg_engine_destroy(mvg_engine* e);
 /* Bit-exact mode (off by default; MVG_EXACT=1 in the environment turns it on at creation):
  * local products by mvg_gemv_exact, and the exchange adds the partials in the reference's own
- * order — the column split's MPI_Reduce as MPICH's binomial tree in rank order
+ * order — the column split's MPI_Reduce as MPICH 3.3.2 sums it (binomial tree, or reduce-scatter
+ * + gather for buffers over 2 KiB, oracle/cpu_ref.c ref_mpich_reduce)
  * (colwise.c:124), the block split's partials into a zeroed y in rank order
  * (blockwise.c:150-207) — after an ncclGather of every partial to rank 0. y is then
  * bit-identical to the reference's (block split with > 2 grid columns: to the reference's

@@ -25,8 +25,9 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 // ----- exact exchange (gemv_exact.hip): the reference's own combine orders on the root
-// MPI_Reduce(SUM) as MPICH's binomial tree in rank order (colwise.c:124); overwrites parts
-int launch_combine_binomial(double* parts, int P, int64_t n, double* y, hipStream_t s);
+// MPI_Reduce(SUM) as the reference's MPICH runs it (colwise.c:124): binomial tree or, for long
+// buffers, reduce-scatter + gather, by MPICH 3.3.2's own rule (gemv_exact.hip); overwrites parts
+int launch_combine_mpich_reduce(double* parts, int P, int64_t n, double* y, hipStream_t s);
 // gather_local_results (blockwise.c:150-207): y = ((0 + p[gi*gc]) + p[gi*gc+1]) + ... per grid row
 int launch_combine_grid_rows(const double* parts, int gr, int gc, int64_t lr, double* y, hipStream_t s);
 

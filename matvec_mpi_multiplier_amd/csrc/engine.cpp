@@ -209,6 +209,19 @@ int h2d_region(double* dst, const double* host, int64_t ld_host, int64_t rows, i
     return MVG_OK;
 }
 
+// A chunked distribution's copies into dA / dx may still be running on the copy stream. Any
+// other writer of those buffers on s.stream (the synthetic fill, the root-send receives) first
+// waits for the last of them (the copy stream runs in order), and the pending chunks are dropped:
+// the next multiply then reads the whole new shard.
+int drain_chunks(Shard& s) {
+    if (s.chunks_pending && !s.chunk_ev.empty()) {
+        const size_t last = s.chunk_row.size() >= 2 ? s.chunk_row.size() - 2 : 0;
+        MVG_HIP(hipStreamWaitEvent(s.stream, s.chunk_ev[last], 0));
+    }
+    s.chunks_pending = false;
+    return MVG_OK;
+}
+
 // x segment that a shard needs: full x (row), strip segment (col), block column segment.
 inline int64_t x_off(const mvg_shard& p) { return p.col_off; }
 inline int64_t x_len(const mvg_shard& p) { return p.n_cols; }
@@ -224,7 +237,7 @@ int distribute_direct(mvg_engine* e, const double* A, const double* x) {
         MVG_HIP(hipSetDevice(s.device));
         const mvg_shard& p = s.plan;
         const int nch = e->overlap_chunks > 1 && p.n_rows >= 2 * (int64_t)e->overlap_chunks ? e->overlap_chunks : 0;
-        s.chunks_pending = false;
+        if (int rc0 = drain_chunks(s); rc0 != MVG_OK) return rc0;
         if (nch == 0) {
             int rc = h2d_region(s.dA, A + p.row_off * C + p.col_off, C, p.n_rows, p.n_cols, s.stream);
             if (rc != MVG_OK) return rc;
@@ -310,7 +323,7 @@ int exchange_exact(mvg_engine* e, int b, bool serial) {
         MVG_HIP(hipSetDevice(s.device));
         hipStream_t st = serial ? s.stream : s.xstream;
         const int rc = e->alg == MVG_ALG_COLWISE
-                           ? launch_combine_binomial(s.gbuf, e->nranks, e->R, s.dy, st)
+                           ? launch_combine_mpich_reduce(s.gbuf, e->nranks, e->R, s.dy, st)
                            : launch_combine_grid_rows(s.gbuf, s.plan.grid_rows, s.plan.grid_cols, s.plan.y_len,
                                                       s.dy, st);
         if (rc != MVG_OK) return rc;
@@ -545,7 +558,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
 // Exact mode: the local products come from mvg_gemv_exact (the reference's sequential sums) and
 // the exchange reproduces the reference's combine order instead of RCCL's: every rank's partial
 // is gathered to rank 0 in rank order (one ncclGather) and a small kernel there adds them as
-// the reference does — MPI_Reduce's binomial tree for the column split (colwise.c:124), the
+// the reference does — MPI_Reduce's tree as MPICH picks it for the column split (colwise.c:124), the
 // grid row's blocks into a zeroed y in rank order for the block split (blockwise.c:150-207).
 // The row split's gather is a copy and stays as it is. y is then bit-identical to the
 // reference's (block split: to its result for rank-order arrival, which is every arrival order
@@ -621,6 +634,7 @@ int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x) {
         s.panels_fresh = false;
         s.uses = 0;
         MVG_HIP(hipSetDevice(s.device));
+        if ((rc = drain_chunks(s)) != MVG_OK) return rc;
         const mvg_shard& p = s.plan;
         if ((rc = mvg_synth_fill_device(s.dA, p.n_cols, p.n_rows, p.n_cols, p.row_off, p.col_off,
                                         e->C, seed_a, s.stream)) != MVG_OK)
@@ -659,7 +673,8 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
         // exactly one local shard
         Shard& s = e->shards[0];
         MVG_HIP(hipSetDevice(s.device));
-        s.chunks_pending = false;  // the root-send form always lands whole shards on s.stream
+        // the root-send form always lands whole shards on s.stream, after any chunked copies
+        if (int rc0 = drain_chunks(s); rc0 != MVG_OK) return rc0;
         // the sends/recvs below use the world communicator on s.stream: order them after any
         // exchange still running on s.xstream (one communicator, one order of operations)
         if (e->x_pending) MVG_HIP(hipStreamWaitEvent(s.stream, s.x_done[(e->nx - 1) % e->ring], 0));

@@ -517,17 +517,33 @@ __global__ __launch_bounds__(64) void gemv_seq_scalar(const double* __restrict__
 }
 
 // ------------------------------------------------------------------ exact combines
-// MPI_Reduce(SUM) as MPICH 3.3 runs it for a commutative op (the reference's colwise.c:124):
-// a binomial tree in rank order, ((p0 + p1) + (p2 + p3)) + ..., parts[r*n + i] = rank r's
-// partial. Overwrites parts; y[i] = the root's result.
-__global__ void combine_binomial(double* __restrict__ parts, int P, int64_t n, double* __restrict__ y) {
+// MPI_Reduce(SUM, root 0) as the reference's MPICH 3.3.2 runs it for a commutative op
+// (colwise.c:124; MPIR_Reduce_intra_auto): with n * 8 > 2048 bytes and n >= pof2 (the largest
+// power of two <= P) reduce-scatter + gather — ranks 2i, 2i+1 (i < rem = P - pof2) fold into new
+// rank i, rank r >= 2 rem becomes new rank r - rem, and the recursive halving sums the pof2 new
+// ranks as a binomial tree — otherwise a binomial tree over all P ranks in rank order,
+// ((p0 + p1) + (p2 + p3)) + .... parts[r*n + i] = rank r's partial; `fold` = rem (0: binomial).
+// Overwrites parts; y[i] = the root's result.
+__global__ void combine_mpich(double* __restrict__ parts, int P, int fold, int64_t n, double* __restrict__ y) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        for (int mask = 1; mask < P; mask <<= 1)
-            for (int r = 0; r + mask < P; r += 2 * mask)
-                parts[r * n + i] = parts[r * n + i] + parts[(r + mask) * n + i];
+        for (int f = 0; f < fold; ++f) parts[2 * f * n + i] = parts[2 * f * n + i] + parts[(2 * f + 1) * n + i];
+        const int m = P - fold;  // ranks left in the tree; new rank k lives in real rank k < fold ? 2k : k + fold
+        for (int mask = 1; mask < m; mask <<= 1)
+            for (int k = 0; k + mask < m; k += 2 * mask) {
+                const int a = k < fold ? 2 * k : k + fold;
+                const int b = k + mask < fold ? 2 * (k + mask) : k + mask + fold;
+                parts[a * n + i] = parts[a * n + i] + parts[b * n + i];
+            }
         y[i] = parts[i];
     }
+}
+
+// rem = P - pof2 when MPICH takes its reduce-scatter + gather algorithm for n doubles, else 0
+int mpich_reduce_fold(int P, int64_t n) {
+    int pof2 = 1;
+    while (pof2 * 2 <= P) pof2 *= 2;
+    return (n * 8 > 2048 && n >= pof2) ? P - pof2 : 0;
 }
 
 // gather_local_results (blockwise.c:150-207): y starts at 0 and every block's partial of the
@@ -546,10 +562,11 @@ __global__ void combine_grid_rows(const double* __restrict__ parts, int gr, int 
     }
 }
 
-int launch_combine_binomial(double* parts, int P, int64_t n, double* y, hipStream_t s) {
+int launch_combine_mpich_reduce(double* parts, int P, int64_t n, double* y, hipStream_t s) {
     if (n <= 0) return MVG_OK;
     const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
-    hipLaunchKernelGGL(combine_binomial, dim3((unsigned)blocks), dim3(256), 0, s, parts, P, n, y);
+    hipLaunchKernelGGL(combine_mpich, dim3((unsigned)blocks), dim3(256), 0, s, parts, P, mpich_reduce_fold(P, n), n,
+                       y);
     MVG_HIP(hipGetLastError());
     return MVG_OK;
 }

@@ -10,9 +10,8 @@
  * -ffp-contract=off (no FMA), exactly the operation order of the reference:
  *   - the local product is a left-to-right sum from 0 (src/matr_utils.c:86-96),
  *   - column split scales in place then row-sums (src/multiplier_colwise.c:107-122) and
- *     combines the strips with MPI_Reduce(SUM) (colwise.c:124), restated as MPICH's
- *     binomial tree over ranks (for commutative ops MPICH 3.3's binomial and
- *     reduce-scatter/gather algorithms both sum ((p0+p1)+(p2+p3))+... in rank order),
+ *     combines the strips with MPI_Reduce(SUM) (colwise.c:124), restated as the image's MPICH
+ *     3.3.2 runs it: binomial tree or reduce-scatter + gather by message size (ref_mpich_reduce),
  *   - block split accumulates y[(src/c)*lr + j] += partial into a zeroed y, the root's own
  *     block first, then the others (src/multiplier_blockwise.c:150-207). The reference takes
  *     them in MPI_ANY_SOURCE arrival order (nondeterministic); this oracle uses rank order.
@@ -54,12 +53,43 @@ int64_t sqrt_floor(int64_t n) {
     return s;
 }
 
-/* MPI_Reduce(SUM) over P rank buffers of n doubles, binomial tree in rank order:
- * at mask = 1, 2, 4, ...: rank r (r % 2mask == 0) adds rank r+mask's buffer. */
-static void binomial_reduce(double** bufs, int P, int64_t n) {
-    for (int mask = 1; mask < P; mask <<= 1)
-        for (int r = 0; r + mask < P; r += 2 * mask)
-            for (int64_t i = 0; i < n; ++i) bufs[r][i] = bufs[r][i] + bufs[r + mask][i];
+/* MPI_Reduce(SUM, root 0) over P rank buffers of n doubles, as the image's MPICH 3.3.2 runs it
+ * for the reference's colwise.c:124 (MPIR_Reduce_intra_auto; on one node the SMP path hands the
+ * same communicator to the same choice):
+ *   - n * 8 > 2048 bytes and n >= pof2 (pof2 = largest power of two <= P): reduce-scatter +
+ *     gather. With rem = P - pof2, ranks 2i and 2i+1 (i < rem) first fold into one new rank i,
+ *     the others become new rank r - rem; the recursive halving then sums the pof2 new ranks as a
+ *     binomial tree ((n0 + n1) + (n2 + n3)) + ...;
+ *   - otherwise the binomial tree over the P ranks: at mask = 1, 2, 4, ... rank r (r % 2mask == 0)
+ *     adds rank r + mask's buffer.
+ * The two agree whenever P is a power of two (and at P = 3, 6, 7, 12); they differ at P = 5, 9,
+ * 10, 11, 13, ... (golden sq_720/colwise/P5, P9, P10 pin both branches). fp64 addition is
+ * commutative bit for bit, so only the association matters. Result in bufs[0]. */
+static void binomial_over(double** bufs, const int* idx, int n_idx, int64_t n) {
+    for (int mask = 1; mask < n_idx; mask <<= 1)
+        for (int r = 0; r + mask < n_idx; r += 2 * mask) {
+            double* a = bufs[idx[r]];
+            const double* b = bufs[idx[r + mask]];
+            for (int64_t i = 0; i < n; ++i) a[i] = a[i] + b[i];
+        }
+}
+
+void ref_mpich_reduce(double** bufs, int P, int64_t n) {
+    int pof2 = 1;
+    while (pof2 * 2 <= P) pof2 *= 2;
+    int* idx = (int*)malloc(sizeof(int) * (size_t)P);
+    int m = P;
+    if (n * 8 > 2048 && n >= pof2 && pof2 != P) {
+        const int rem = P - pof2;
+        for (int i = 0; i < rem; ++i)
+            for (int64_t k = 0; k < n; ++k) bufs[2 * i][k] = bufs[2 * i][k] + bufs[2 * i + 1][k];
+        for (int i = 0; i < pof2; ++i) idx[i] = i < rem ? 2 * i : i + rem;
+        m = pof2;
+    } else {
+        for (int i = 0; i < P; ++i) idx[i] = i;
+    }
+    binomial_over(bufs, idx, m, n);
+    free(idx);
 }
 
 /* src/multiplier_rowwise.c:93,139-141: scatter rows, local product, gather in rank order.
@@ -92,7 +122,7 @@ int ref_colwise(const double* A, const double* x, int64_t R, int64_t C, int P, d
             part[p][i] = sum;
         }
     }
-    binomial_reduce(part, P, R); /* :124 */
+    ref_mpich_reduce(part, P, R); /* :124 */
     memcpy(y, part[0], sizeof(double) * (size_t)R);
     for (int p = 0; p < P; ++p) free(part[p]);
     free(part);
@@ -224,7 +254,7 @@ static void* rank_main(void* arg) {
             if (j->alg == 0) {
                 for (int p = 0; p < P; ++p) memcpy(j->y + p * lr, j->parts[p], sizeof(double) * (size_t)lr);
             } else if (j->alg == 1) {
-                binomial_reduce(j->parts, P, R);
+                ref_mpich_reduce(j->parts, P, R);
                 memcpy(j->y, j->parts[0], sizeof(double) * (size_t)R);
             } else {
                 for (int64_t i = 0; i < R; ++i) j->y[i] = 0.0;

@@ -7,6 +7,7 @@ void ref_multiply_std_rowwise(const double* matrix, const double* vector, int64_
                               int64_t n_cols, double* result);
 void ref_grid_shape(int64_t number, int* dividers);
 int64_t sqrt_floor(int64_t n);
+void ref_mpich_reduce(double** bufs, int P, int64_t n);
 int ref_rowwise(const double* A, const double* x, int64_t R, int64_t C, int P, double* y);
 int ref_colwise(const double* A, const double* x, int64_t R, int64_t C, int P, double* y);
 int ref_blockwise(const double* A, const double* x, int64_t R, int64_t C, int P, double* y);

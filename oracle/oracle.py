@@ -40,6 +40,8 @@ def _load() -> C.CDLL:
     lib.ref_synth_block.restype = None
     lib.ref_time_multiply.argtypes = [C.c_int, dp, dp, C.c_int64, C.c_int64, C.c_int, C.c_int, dp]
     lib.ref_time_multiply.restype = C.c_double
+    lib.ref_mpich_reduce.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int64]
+    lib.ref_mpich_reduce.restype = None
     return lib
 
 
@@ -68,6 +70,17 @@ def multiply(alg: str, A: np.ndarray, x: np.ndarray, P: int) -> np.ndarray:
     if rc != 0:
         raise ValueError(f"oracle: {alg} {R}x{Cn} does not split over P={P}")
     return y[:R]
+
+
+def mpich_reduce(parts: list[np.ndarray]) -> np.ndarray:
+    """MPI_Reduce(SUM, root 0) of the ranks' partial y in the order the reference's MPICH 3.3.2
+    sums them (multiplier_colwise.c:124; binomial tree, or reduce-scatter + gather above 2 KiB,
+    oracle/cpu_ref.c ref_mpich_reduce)."""
+    bufs = [_c(p).copy() for p in parts]
+    n = bufs[0].shape[0]
+    ptrs = (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+    lib.ref_mpich_reduce(ptrs, len(bufs), n)
+    return bufs[0]
 
 
 def grid_shape(p: int) -> tuple[int, int]:

@@ -37,7 +37,12 @@ CASES = [
     ("fixture_4x8", 4, 8, "fixture", {"rowwise": [1, 2, 4], "colwise": [1, 2, 4, 8], "blockwise": [1, 2, 4, 8]}),
     ("odd_5x7", 5, 7, "synth", {"rowwise": [1, 5], "colwise": [1, 7], "blockwise": [1, 7]}),
     ("sq_480", 480, 480, "synth", {a: [1, 2, 3, 4, 6, 8] for a in ALL}),
-    ("wide_120x6000", 120, 6000, "synth", {a: [1, 2, 4, 8] for a in ALL}),
+    # colwise P = 5, 6 at R = 120: MPICH's binomial MPI_Reduce (120 * 8 bytes <= 2048)
+    ("wide_120x6000", 120, 6000, "synth", {"rowwise": [1, 2, 4, 8], "colwise": [1, 2, 4, 5, 6, 8],
+                                           "blockwise": [1, 2, 4, 8]}),
+    # colwise at non-power-of-two P with R = 720 (> 2048 bytes): MPICH's reduce-scatter + gather
+    # MPI_Reduce, whose sum order differs from the binomial tree's at P = 5, 9, 10 (3, 6, 12 agree)
+    ("sq_720", 720, 720, "synth", {"colwise": [1, 2, 3, 5, 6, 8, 9, 10, 12]}),
     # column split is left out for R > C: the reference corrupts its heap there
     # (multiplier_colwise.c:115 sizes `columns` by n_cols, SURVEY §4 bug 2).
     ("tall_960x96", 960, 96, "synth", {"rowwise": [1, 2, 4, 8], "blockwise": [1, 2, 3, 4, 8]}),

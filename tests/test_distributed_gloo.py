@@ -32,6 +32,14 @@ CASES = [
     ("sq_480", 480, 480, "blockwise", 4, True),
     ("wide_120x6000", 120, 6000, "blockwise", 4, True),
     ("tall_960x96", 960, 96, "rowwise", 4, True),
+    # world size 8: the column split's 8 strips and the block split's 2 x 4 grid (config 4's
+    # grid, utils.c:26-37): grid-row Reduce over 4 ranks, then the leaders' Gather
+    # (multiplier_blockwise.c:144-210)
+    ("fixture_4x8", 4, 8, "colwise", 8, False),
+    ("fixture_4x8", 4, 8, "blockwise", 8, False),
+    ("sq_480", 480, 480, "rowwise", 8, True),
+    ("sq_480", 480, 480, "colwise", 8, False),
+    ("sq_480", 480, 480, "blockwise", 8, False),
 ]
 
 
@@ -187,8 +195,9 @@ def test_shared_host_matrix_two_ranks(stale):
 def _exact_worker(rank, world, port, case, R, C, alg, outq):
     """The exact-mode exchange (engine.cpp exchange_exact) over gloo: every rank's partial
     gathered to rank 0 in rank order, then added there in the reference's order — MPICH's
-    binomial MPI_Reduce for the column split, the grid row's partials into a zeroed y in rank
-    order for the block split (the order of the combine kernels in csrc/gemv_exact.hip)."""
+    MPI_Reduce tree for the column split (binomial, or reduce-scatter + gather for buffers over
+    2 KiB), the grid row's partials into a zeroed y in rank order for the block split (the order
+    of the combine kernels in csrc/gemv_exact.hip)."""
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -208,12 +217,7 @@ def _exact_worker(rank, world, port, case, R, C, alg, outq):
         if rank == 0:
             parts = [g.numpy().copy() for g in gl]
             if alg == "colwise":
-                mask = 1
-                while mask < world:
-                    for r in range(0, world - mask, 2 * mask):
-                        parts[r] = parts[r] + parts[r + mask]
-                    mask *= 2
-                y = parts[0]
+                y = oracle.mpich_reduce(parts)
             else:
                 gr, gc = mm.get_2_most_closest_multipliers(world)
                 lr = R // gr
@@ -225,12 +229,23 @@ def _exact_worker(rank, world, port, case, R, C, alg, outq):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,R,C,alg,P", [("fixture_4x8", 4, 8, "colwise", 4), ("sq_480", 480, 480, "colwise", 4),
-                                            ("sq_480", 480, 480, "colwise", 3), ("sq_480", 480, 480, "blockwise", 4),
-                                            ("wide_120x6000", 120, 6000, "blockwise", 2)])
+@pytest.mark.parametrize("case,R,C,alg,P", [
+    ("fixture_4x8", 4, 8, "colwise", 4), ("sq_480", 480, 480, "colwise", 4), ("sq_480", 480, 480, "colwise", 3),
+    ("sq_480", 480, 480, "blockwise", 4), ("wide_120x6000", 120, 6000, "blockwise", 2),
+    # world size 8 (config 3's largest P, config 4's 2 x 4 grid)
+    ("fixture_4x8", 4, 8, "colwise", 8), ("sq_480", 480, 480, "colwise", 8), ("fixture_4x8", 4, 8, "blockwise", 8),
+    ("sq_480", 480, 480, "blockwise", 8),
+    # MPICH's reduce-scatter + gather order (R * 8 > 2048 bytes) where it differs from the
+    # binomial tree, and the binomial tree at a non-power-of-two P for a short y
+    ("sq_720", 720, 720, "colwise", 5), ("sq_720", 720, 720, "colwise", 10), ("wide_120x6000", 120, 6000, "colwise", 5),
+])
 def test_gloo_exact_exchange_is_bit_identical_to_reference(golden, case, R, C, alg, P):
     # where the RCCL/gloo reduce differs from MPICH in the last bit (the replay above at P = 4),
-    # the exact exchange gives the reference's own bits
+    # the exact exchange gives the reference's own bits; a block split over more than two grid
+    # columns adds in the reference's message-arrival order (blockwise.c:187,206): there the
+    # exchange gives the oracle's rank order bit for bit and the reference's y within 1e-15
+    from oracle import oracle
+
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -241,4 +256,10 @@ def test_gloo_exact_exchange_is_bit_identical_to_reference(golden, case, R, C, a
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    np.testing.assert_array_equal(y, golden[f"{case}/{alg}/P{P}"])
+    want = golden[f"{case}/{alg}/P{P}"]
+    if alg == "blockwise" and oracle.grid_shape(P)[1] > 2:
+        A, x = _inputs(case, R, C)
+        np.testing.assert_array_equal(y, oracle.multiply(alg, A, x, P))
+        assert max_rel(y, want) <= 1e-15
+    else:
+        np.testing.assert_array_equal(y, want)
