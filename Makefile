@@ -72,8 +72,32 @@ bin/multiplier_blockwise: $(APP_DEPS) | $(BUILD)
 oracle:
 	$(MAKE) -C oracle
 
+# ---- the host code under AddressSanitizer + UndefinedBehaviorSanitizer, on the CPU only
+# (SURVEY §5): the library's host translation units (planner, engine, text loader) and the
+# oracle, built with the ROCm clang (host code; the kernels' objects are linked unchanged), then
+# the CPU tests that drive them (tools/asan_tests.sh). Nothing here runs on a GPU.
+ASAN_DIR := $(BUILD)/asan
+CLANGXX  := $(ROCM)/lib/llvm/bin/clang++
+CLANGC   := $(ROCM)/lib/llvm/bin/clang
+SANFLAGS := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+ASAN_OBJS := $(ASAN_DIR)/host.o $(ASAN_DIR)/engine.o $(ASAN_DIR)/textio.o
+
+asan: $(ASAN_DIR)/libmatvec_gpu.so $(ASAN_DIR)/liboracle.so
+
+$(ASAN_DIR):
+	mkdir -p $(ASAN_DIR)
+
+$(ASAN_DIR)/%.o: $(CSRC)/%.cpp $(HDRS) | $(ASAN_DIR)
+	$(CLANGXX) -std=c++17 -fPIC -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include $(SANFLAGS) -c $< -o $@
+
+$(ASAN_DIR)/libmatvec_gpu.so: $(ASAN_OBJS) $(BUILD)/gemv.o $(BUILD)/gemv_exact.o
+	$(CLANGXX) -shared -fPIC -shared-libasan $(SANFLAGS) $(BUILD)/gemv.o $(BUILD)/gemv_exact.o $(ASAN_OBJS) -o $@ $(LDLIBS)
+
+$(ASAN_DIR)/liboracle.so: oracle/cpu_ref.c oracle/cpu_ref.h | $(ASAN_DIR)
+	$(CLANGC) -std=c11 -fPIC -shared -shared-libasan -ffp-contract=off -pthread $(SANFLAGS) $< -o $@
+
 clean:
 	rm -rf $(BUILD) $(LIB) $(LAUNCH) $(APPS) $(EXAMPLES)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle examples
+.PHONY: all clean oracle examples asan

@@ -22,6 +22,9 @@
 //   MVG_ITERS=n        timed iterations (default 100, as the reference's loop, rowwise.c:135)
 //   MVG_SYNTH=1        skip the text files and generate the synthetic inputs (spec in
 //                      include/matvec_gpu.h) on the host — the large configs have no files
+//   MVG_SYNTH=device   generate each rank's shard of the same inputs on its GPU instead (no host
+//                      A: config 4's 137 GB never exists on the host); nothing is distributed, so
+//                      the timed loop is multiply + y on the root
 //   MVG_Y_OUT=path     write y, "%.17g" per line (the reference never writes y)
 //   MVG_EXACT=1        bit-exact mode (mvg_engine_set_exact): y, and so the MVG_Y_OUT file, is
 //                      identical to the reference's (its sequential sums and combine orders)
@@ -81,6 +84,9 @@ static int fatal(int rc, const char* where) {
 
 int main(int argc, char** argv) {
     const int alg = MVG_APP_ALG;
+    // one process per GPU: RCCL's intra-node IPC on this ROCm needs the dmabuf mode (the legacy
+    // IPC handles fail with hipIpcGetMemHandle: invalid argument); before the HIP runtime starts
+    setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);
     if (argc < 3) {  // the reference dereferences argv[1..2] unchecked (rowwise.c:58-59)
         fprintf(stderr, "usage: %s <n_rows> <n_cols>\n", argv[0]);
         return 1;
@@ -181,8 +187,10 @@ int main(int argc, char** argv) {
     // The root's A and x: in rank mode on one node, an MPI-3 shared window every rank maps (A,
     // then x); otherwise the root's own memory.
     const size_t nA = (size_t)n_rows * (size_t)n_cols;
+    const char* synth_env = getenv("MVG_SYNTH");
+    const bool synth_device = synth_env && strcmp(synth_env, "device") == 0;
     const char* dist_env = getenv("MVG_DIST");
-    const bool want_shared = ranks && !(dist_env && strcmp(dist_env, "send") == 0);
+    const bool want_shared = ranks && !synth_device && !(dist_env && strcmp(dist_env, "send") == 0);
     double* shared = want_shared ? (double*)launch_shared_alloc((nA + (size_t)n_cols + 1) * sizeof(double)) : nullptr;
     std::vector<double> x_own, y(root ? std::max(n_rows, 1L) : 1);
     std::unique_ptr<double, decltype(&free)> A_own(nullptr, &free);
@@ -198,7 +206,7 @@ int main(int argc, char** argv) {
         (void)mvg_host_first_touch(A + r0 * n_cols, (size_t)(r1 - r0) * (size_t)n_cols * sizeof(double),
                                    my_device);
         launch_barrier();
-    } else if (root || !ranks) {
+    } else if (!synth_device && (root || !ranks)) {
         // left untouched by the allocation: the first write decides each page's NUMA node
         A_own.reset((double*)malloc(std::max<size_t>(nA, 1) * sizeof(double)));
         if (!A_own) {
@@ -218,7 +226,10 @@ int main(int argc, char** argv) {
     }
     if (root) {
         char name[128];
-        if (env_long("MVG_SYNTH", 0)) {
+        if (synth_device) {
+            printf("Generating synthetic matrix %ld x %ld (seed %u) and vector (seed %u) on the GPUs...\n", n_rows,
+                   n_cols, MVG_SEED_A, MVG_SEED_X);
+        } else if (env_long("MVG_SYNTH", 0)) {
             printf("Generating synthetic matrix %ld x %ld (seed %u) and vector (seed %u)...\n", n_rows, n_cols,
                    MVG_SEED_A, MVG_SEED_X);
             if ((rc = mvg_synth_fill_host(A, n_cols, n_rows, n_cols, 0, 0, n_cols, MVG_SEED_A)) != MVG_OK ||
@@ -291,7 +302,10 @@ int main(int argc, char** argv) {
     if ((rc = mvg_engine_create(&eng, alg, n_rows, n_cols, comm)) != MVG_OK)
         return fatal(rc, "mvg_engine_create");
 
+    if (synth_device && (rc = mvg_engine_fill_synth(eng, MVG_SEED_A, MVG_SEED_X)) != MVG_OK)
+        return fatal(rc, "mvg_engine_fill_synth");
     auto distribute = [&]() {
+        if (synth_device) return (int)MVG_OK;  // the shards were generated in place
         if (shared) return mvg_engine_distribute_shared(eng, A, x);
         return mvg_engine_distribute(eng, root ? A : nullptr, root ? x : nullptr);
     };
@@ -330,14 +344,17 @@ int main(int argc, char** argv) {
     if (root) {
         const double bytes =
             8.0 * ((double)nA + (double)n_cols * (alg == MVG_ALG_ROWWISE ? comm_sz : 1) + (double)n_rows);
-        printf("end-to-end (distribute + multiply + y on root): mean %.6f s over %ld iterations\n",
+        printf("end-to-end (%s): mean %.6f s over %ld iterations\n",
+               synth_device ? "multiply + y on root; inputs generated on the GPUs, nothing distributed"
+                            : "distribute + multiply + y on root",
                sum_time / iters, iters);
         printf("device-resident: %.4f ms per multiply, %.1f GB/s aggregate; GEMV kernel %.3f ms (max over GPUs)\n",
                dev_s * 1e3, bytes / dev_s / 1e9, kms);
         if (ranks)
             printf("launch: %d ranks, one GPU each; distribution %s\n", comm_sz,
-                   shared ? "from the root's A in a node-shared window, every GPU over its own link"
-                          : "root H2D staging + ncclSend over xGMI");
+                   synth_device ? "none (inputs generated on every GPU)"
+                   : shared     ? "from the root's A in a node-shared window, every GPU over its own link"
+                                : "root H2D staging + ncclSend over xGMI");
         if (const char* tl = getenv("MVG_ITER_LOG")) {  // per-iteration end-to-end times, seconds
             if (FILE* f = fopen(tl, "w")) {
                 for (double t : it_times) fprintf(f, "%.9f\n", t);

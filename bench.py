@@ -67,6 +67,13 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs 3-5 section")
     ap.add_argument("--configs", default="3,4,5", help="which BASELINE configs the section runs, in order")
     ap.add_argument("--config-steps", type=int, default=20)
+    ap.add_argument("--no-config-cpu-baseline", action="store_true",
+                    help="skip the per-config CPU baselines (configs 3-5, N = 1)")
+    ap.add_argument("--config-ref-rows", type=int, default=128,
+                    help="rows of each config's slice the real reference runs on")
+    ap.add_argument("--config-cpu-sample-bytes", type=float, default=3.5e10,
+                    help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
+    ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the bit-exact section (the same workload with mvg_engine_set_exact)")
     return ap.parse_args()
@@ -96,6 +103,15 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
+    # one process per GPU: CUDA-tensor / RCCL IPC between processes needs the dmabuf IPC mode on
+    # this ROCm (the legacy handle path fails with hipIpcGetMemHandle: invalid argument); set before
+    # the HIP runtime starts. With N > 1, RCCL logs its transport choices to a per-rank file that
+    # rccl_report() reads back (P2P/IPC over xGMI, or SHM / NET), unless the caller set NCCL_DEBUG.
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    rccl_log = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG" not in os.environ:
+        rccl_log = f"/tmp/mvg_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log"
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=rccl_log)
     import torch
     import torch.distributed as dist
 
@@ -194,13 +210,18 @@ def main():
     # ---- CPU baseline: rank 0 at N = 1 only
     cpu = None
     if rank == 0 and n == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, R, C, y, y_exact)
+        cpu = cpu_baseline(args, args.alg, R, C, y, y_exact)
         same_port, same_ref = cpu.pop("exact_vs_port", None), cpu.pop("exact_vs_reference", None)
         if exact is not None:
             # rowwise: the exact y against the oracle port's y (full matrix) and against the real
             # reference's own y (its sample rows), bit for bit
             exact["bit_identical_to_port"] = same_port
             exact["bit_identical_to_reference_sample"] = same_ref
+
+    rccl = rccl_report(rccl_log, distributed, rank) if distributed else None
+    ref_rows = None
+    if rank == 0 and args.alg == "rowwise" and (R, C) == (SHARD, SHARD):
+        ref_rows = reference_rows_check("config 2", "rowwise", R, C, n, y, y_exact)
 
     if rank == 0:
         traffic, traffic_src = pmc_traffic(args.alg, R, C, n)
@@ -240,6 +261,8 @@ def main():
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
+            "reference_rows": ref_rows,
+            "rccl": rccl,
             "exact": exact,
             "end_to_end": e2e,
             "configs": configs,
@@ -261,12 +284,12 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
     import torch
     import torch.distributed as dist
 
-    eng.set_exact(True)
-    try:
+    steps = max(10, args.steps // 2)
+
+    def run_exact():
         for _ in range(max(2, args.warmup // 4)):
             eng.multiply()
         eng.sync()
-        steps = max(10, args.steps // 2)
         eng.kernel_timing(args.event_every)
         barrier()
         t0 = time.perf_counter()
@@ -281,19 +304,45 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
         if distributed:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kms = float(t[0]), float(t[1])
-        y = eng.collect()
-        kernel = exact_kernel_name(eng)
+        return el, kms, eng.collect(), exact_kernel_name(eng)
+
+    # 1) repeated multiplies of one distribution (the bench's step): from the second multiply on,
+    #    the engine's column-panel copy of the shard (rebuilt once, during the warmup)
+    eng.set_exact(True)
+    try:
+        el, kms, y, kernel = run_exact()
     finally:
         eng.set_exact(False)
-    out = {"semantics": "mvg_engine_set_exact: y bit-identical to the reference's sequential sums",
+    # 2) the row-major exact kernels, which every multiply of a fresh distribution runs (the
+    #    drop-in executables: distribute + multiply each iteration, MVG_EXACT=1)
+    had = os.environ.get("MVG_NO_PANELS")
+    os.environ["MVG_NO_PANELS"] = "1"
+    eng.set_exact(True)
+    try:
+        rel_, rkms, y_rm, rkernel = run_exact()
+    finally:
+        eng.set_exact(False)
+        if had is None:
+            del os.environ["MVG_NO_PANELS"]
+        else:
+            os.environ["MVG_NO_PANELS"] = had
+    frac = (lambda ms: round(per_gpu / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if ms > 0 else None)
+    out = {"semantics": "mvg_engine_set_exact: y bit-identical to the reference's sequential sums; "
+                        "repeated multiplies of one distribution (device-resident), which run on the "
+                        "engine's column-panel copy of the shard from the second multiply on (built "
+                        "during the warmup, DESIGN.md §4b); `row_major`: the kernels a fresh "
+                        "distribution runs (the executables' MVG_EXACT=1 loop)",
            "value": round(total_bytes * steps / el / 1e9, 1), "unit": "GB/s", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4), "gflops": round(2 * eng.R * eng.C * steps / el / 1e9, 1),
            "kernel": kernel,
            "kernel_ms": round(kms, 5),
-           "roofline_frac": round(per_gpu / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None}
+           "roofline_frac": frac(kms),
+           "row_major": {"value": round(total_bytes * steps / rel_ / 1e9, 1), "ms_per_step": round(rel_ / steps * 1e3, 4),
+                         "kernel": rkernel, "kernel_ms": round(rkms, 5), "roofline_frac": frac(rkms)}}
     if rank == 0:
         rel = float(np.max(np.abs(y - y_tree) / np.abs(y_tree)))
         assert rel <= 1e-12, f"exact y differs from the tree-summed y by {rel}"
+        assert np.array_equal(y, y_rm), "the panel and row-major exact kernels differ"
         out["max_rel_vs_tree"] = rel
     return out, y
 
@@ -369,6 +418,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             e.sync()
             el, kms = timed(e, args.config_steps)
             y = e.collect()
+            yx = None
             if rank == 0:
                 assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range"
             if not args.no_exact:
@@ -394,7 +444,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
         finally:
             e.destroy()
         gr, gc = mm.get_2_most_closest_multipliers(n)
-        out.append({
+        entry = {
             "config": name, "alg": alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
             "grid": [gr, gc] if alg == "blockwise" else None,
             "value": round(total * args.config_steps / el / 1e9, 1), "unit": "GB/s",
@@ -403,8 +453,98 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             "kernel": kernel_name(sh), "kernel_ms": round(kms, 5),
             "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
             "exact": exact,
-        })
+        }
+        if rank == 0:
+            entry["reference_rows"] = reference_rows_check(name, alg, R, C, n, y, yx)
+            if n == 1 and not args.no_cpu_baseline and not args.no_config_cpu_baseline:
+                # the reference on a leading-row slice at the host's core count, and the -O2 port
+                # on the whole config where host memory allows (config 4: its leading rows)
+                try:
+                    entry["cpu_baseline"] = cpu_baseline(args, alg, R, C, y, None, ref_rows=args.config_ref_rows,
+                                                         sample_bytes=args.config_cpu_sample_bytes,
+                                                         cpu_seconds=args.config_cpu_seconds, placements=("spread",))
+                except Exception as exc:  # the baseline must never sink the bench
+                    entry["cpu_baseline"] = f"failed: {str(exc)[:300]}"
+        out.append(entry)
+        del y, yx
     return out
+
+
+SLICES = os.path.join(REPO, "tests", "golden", "config_slices.npz")
+
+
+def reference_rows_check(name, alg, R, C, n, y, yx):
+    """The config's y on the rows the real reference computed at the same (R, C, P = n)
+    (tests/golden/config_slices.npz: oracle/_ref under mpiexec -n P on four bands of the config's
+    rows, which is the reference's y for those rows of the full problem). Tree form: <= 1e-12
+    (asserted); exact form: bit-identical except the block split over more than two grid columns,
+    whose reference sum follows message arrival order."""
+    key_cfg = "cfg" + name.split()[-1]
+    if not os.path.exists(SLICES):
+        return None
+    with np.load(SLICES) as z:
+        if f"{key_cfg}/{alg}/P{n}" not in z.files:
+            return {"P": n, "checked": False, "why": f"no reference slice for P = {n}"}
+        rows, want = z[f"{key_cfg}/rows"], z[f"{key_cfg}/{alg}/P{n}"]
+    rel = float(np.max(np.abs(y[rows] - want) / np.abs(want)))
+    assert rel <= 1e-12, f"{name}: y differs from the reference's own y on its rows by {rel}"
+    out = {"P": n, "rows": int(len(rows)), "max_rel": rel,
+           "source": "tests/golden/config_slices.npz: oracle/_ref, mpiexec -n P, on 4 bands of the config's rows"}
+    if yx is not None:
+        gc = mm_grid_cols(n) if alg == "blockwise" else 1
+        out["exact_bit_identical"] = bool(np.array_equal(yx[rows], want))
+        out["exact_max_rel"] = float(np.max(np.abs(yx[rows] - want) / np.abs(want)))
+        if gc > 2:
+            out["exact_note"] = "grid of > 2 columns: the reference adds in message-arrival order"
+    return out
+
+
+def mm_grid_cols(n):
+    from matvec_mpi_multiplier_amd import multiplier as mm
+
+    return mm.get_2_most_closest_multipliers(n)[1]
+
+
+def rccl_report(path, distributed, rank):
+    """What RCCL reported about its communicators, all ranks gathered on rank 0: the transport of
+    every connection it set up ("a->b": P2P/IPC, P2P/direct pointer, SHM, NET/...), counted per
+    transport, and the communicator sizes (nranks) it initialised. Parsed from the NCCL_DEBUG=INFO
+    file each rank wrote (NCCL_DEBUG_FILE); None when the caller set NCCL_DEBUG itself."""
+    import re
+
+    import torch.distributed as dist
+
+    mine = {"links": {}, "nranks": []}
+    if path and os.path.exists(path):
+        pat = re.compile(r"(\d+)\[\d+\] -> (\d+)\[\d+\](?: \[(?:send|receive)\])? via (\S+)")
+        for line in open(path, errors="replace"):
+            m = pat.search(line)
+            if m:
+                mine["links"].setdefault(f"{m.group(1)}->{m.group(2)}", set()).add(m.group(3))
+            m = re.search(r"nranks (\d+)", line)
+            if m and "Init COMPLETE" in line:
+                mine["nranks"].append(int(m.group(1)))
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+    mine["links"] = {k: sorted(v) for k, v in mine["links"].items()}
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, mine)
+    if rank != 0:
+        return None
+    if path is None:
+        return {"logged": False, "why": "NCCL_DEBUG set by the caller"}
+    links, counts, sizes = {}, {}, set()
+    for r in allr:
+        sizes.update(r["nranks"])
+        for k, v in r["links"].items():
+            links.setdefault(k, set()).update(v)
+    for v in links.values():
+        for t in v:
+            counts[t] = counts.get(t, 0) + 1
+    return {"logged": True, "comm_sizes": sorted(sizes), "transport_counts": counts,
+            "links": {k: sorted(v) for k, v in sorted(links.items())}}
 
 
 def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_bytes, local):
@@ -532,26 +672,28 @@ def pcie_roofline(local):
     return out
 
 
-def cpu_baseline(args, R, C, y_gpu, y_exact=None):
+def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_bytes=None, cpu_seconds=None,
+                 placements=("spread", "compact")):
     """The reference's CPU path timed on this host. Preferred: the real reference (oracle/_ref,
     built from its own sources, run with MPICH's mpiexec on P = the port's thread count) on the
-    leading --ref-rows rows of the same matrix, kind "reference"; its 100-iteration loop is fixed
+    leading `ref_rows` rows of the same matrix, kind "reference"; its 100-iteration loop is fixed
     in its source. Always also: the oracle port (below), reported under "port" (or as the
     baseline itself, kind "port", when the reference cannot run here)."""
-    port = cpu_port_baseline(args, R, C, y_gpu, y_exact)
+    ref_rows = args.ref_rows if ref_rows is None else ref_rows
+    port = cpu_port_baseline(args, alg, R, C, y_gpu, y_exact, sample_bytes, cpu_seconds)
     if args.no_ref_baseline:
         return port
     from oracle import ref_runner
 
     P = port["cores"]
     cpus = port["placement"]["cpus"]
-    rows = min(R, args.ref_rows)
-    if args.alg in ("rowwise", "blockwise"):
+    rows = min(R, ref_rows)
+    if alg in ("rowwise", "blockwise"):
         from oracle import oracle
 
-        gr = P if args.alg == "rowwise" else oracle.grid_shape(P)[0]
+        gr = P if alg == "rowwise" else oracle.grid_shape(P)[0]
         rows = max(gr, rows - rows % gr)
-    if not ref_runner.available(args.alg) or not _splits(args.alg, rows, C, P):
+    if not ref_runner.available(alg) or not _splits(alg, rows, C, P):
         port["reference"] = "not run: oracle/_ref or mpiexec absent, or the sample does not split"
         return port
     # the reference is communication-bound (its root scatters A through MPI shared memory every
@@ -560,9 +702,12 @@ def cpu_baseline(args, R, C, y_gpu, y_exact=None):
     from oracle import cpuset
 
     runs = []
-    for label, cset in (("spread", cpus), ("compact", cpuset.pick_compact(P, gpu_numa_node()))):
+    sets = {"spread": cpus, "compact": None}
+    for label in placements:
+        cset = sets[label] if sets[label] is not None else cpuset.pick_compact(P, gpu_numa_node())
         try:
-            runs.append((label, cset, ref_runner.run(args.alg, rows, C, P, timeout=args.ref_timeout, cpus=cset)))
+            runs.append((label, cset, ref_runner.run(alg, rows, C, P, timeout=args.ref_timeout, cpus=cset,
+                                                     rows=np.arange(rows))))
         except Exception as exc:  # the baseline must never sink the bench
             port.setdefault("reference_errors", []).append(f"{label}: {str(exc)[:200]}")
     if not runs:
@@ -575,7 +720,7 @@ def cpu_baseline(args, R, C, y_gpu, y_exact=None):
     nbytes = 8 * (rows * C + C + rows)
     return {"value": round(nbytes / r["seconds"] / 1e9, 3), "unit": "GB/s", "cores": P, "kind": "reference",
             "ms_per_step": round(r["seconds"] * 1e3, 3), "iters": 100,
-            "sample": f"leading {rows} of {R} rows ({rows}x{C}) {args.alg}: the reference's own executable "
+            "sample": f"leading {rows} of {R} rows ({rows}x{C}) {alg}: the reference's own executable "
                       f"(oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its text inputs, its "
                       f"100-iteration loop (distribution from the root + sequential sums + collection); "
                       f"run {r['wall_s']:.1f} s incl. text loading; GPU y matches its y to {rel:.1e}",
@@ -583,28 +728,32 @@ def cpu_baseline(args, R, C, y_gpu, y_exact=None):
             "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")},
             "exact_vs_port": port.get("exact_vs_port"),
             **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}
-               if y_exact is not None and args.alg == "rowwise" else {})}
+               if y_exact is not None and alg == "rowwise" else {})}
 
 
-def cpu_port_baseline(args, R, C, y_gpu, y_exact=None):
+def cpu_port_baseline(args, alg, R, C, y_gpu, y_exact=None, sample_bytes=None, cpu_seconds=None):
     """The oracle restatement of the reference's CPU path (P threads as MPI ranks, distribution
     from the root's A included, mean of per-iteration max) on this host, on the full workload
-    or, above --cpu-sample-bytes, on its leading rows (same values, same algorithm)."""
+    or, above `sample_bytes`, on its leading rows (same values, same algorithm)."""
+    from matvec_mpi_multiplier_amd import multiplier as mm
     from oracle import oracle
 
+    sample_bytes = args.cpu_sample_bytes if sample_bytes is None else sample_bytes
+    cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
     threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     rows = R
-    if R * C * 8 > args.cpu_sample_bytes:
-        rows = max(1, int(args.cpu_sample_bytes // (C * 8)))
+    if R * C * 8 > sample_bytes:
+        rows = max(1, int(sample_bytes // (C * 8)))
     # keep the sample splittable the way the algorithm splits it over `threads` ranks: sampled
     # rows are rounded down to a multiple of the ranks over rows; the column split (fixed C)
     # lowers the rank count instead
-    if rows < R and args.alg in ("rowwise", "blockwise"):
-        gr = oracle.grid_shape(threads)[0] if args.alg == "blockwise" else threads
+    if rows < R and alg in ("rowwise", "blockwise"):
+        gr = oracle.grid_shape(threads)[0] if alg == "blockwise" else threads
         rows = max(gr, rows - rows % gr)
-    while threads > 1 and not _splits(args.alg, rows, C, threads):
+    while threads > 1 and not _splits(alg, rows, C, threads):
         threads -= 1
-    A = oracle.synth_block(0, rows, 0, C, C, 42)
+    # the inputs (not the timed path): the library's threaded generator of the same values
+    A = mm.synth_host(rows, C, 42)
     x = oracle.synth(1, C, 4242)[0]
     # `cores` is enforced, not assumed: the port's threads (and the reference's ranks after it)
     # run confined to exactly `threads` CPUs, those of the GPU's NUMA node first
@@ -613,13 +762,14 @@ def cpu_port_baseline(args, R, C, y_gpu, y_exact=None):
     cpus = cpuset.pick(threads, gpu_numa_node())
     threads = len(cpus)
     with cpuset.confined(cpus):
-        t1, y_cpu = oracle.time_multiply(args.alg, A, x, threads, 1)
-        iters = max(2, min(200, int(args.cpu_seconds / max(t1, 1e-6))))
-        t, y_cpu = oracle.time_multiply(args.alg, A, x, threads, iters)
+        t1, y_cpu = oracle.time_multiply(alg, A, x, threads, 1)
+        iters = max(2, min(200, int(cpu_seconds / max(t1, 1e-6))))
+        t, y_cpu = oracle.time_multiply(alg, A, x, threads, iters)
+    del A
     rel = float(np.max(np.abs(y_gpu[:rows] - y_cpu) / np.abs(y_cpu)))
     assert rel <= 1e-12, f"GPU y differs from the reference restatement: {rel}"
     exact_same = None
-    if y_exact is not None and args.alg == "rowwise":
+    if y_exact is not None and alg == "rowwise":
         # row sums do not depend on the rank count, so the port's P-rank y is the reference's y
         # for the GPU's single shard too; the exact mode must reproduce it bit for bit (the
         # column and block splits' combine orders depend on P, and the GPU runs P = N here)
@@ -630,9 +780,9 @@ def cpu_port_baseline(args, R, C, y_gpu, y_exact=None):
     return {"exact_vs_port": exact_same, "value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port",
             "ms_per_step": round(t * 1e3, 3), "iters": iters,
-            "sample": f"{what} ({rows}x{C}) {args.alg}, {threads} threads as ranks, {iters} iterations "
+            "sample": f"{what} ({rows}x{C}) {alg}, {threads} threads as ranks, {iters} iterations "
                       f"(reference timing semantics: distribution from the root's A + sequential sums + "
-                      f"collection, max over ranks); GPU y matches to {rel:.1e}",
+                      f"collection, max over ranks; gcc -O2); GPU y matches to {rel:.1e}",
             "host_cpu": host_cpu(), "placement": {"cpus": cpus, "record": cpuset.describe(cpus)}}
 
 

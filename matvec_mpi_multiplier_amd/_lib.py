@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmatvec_gpu.so")
+# MVG_LIB: another build of the same library (the sanitizer build, `make asan`)
+LIB_PATH = os.environ.get("MVG_LIB") or os.path.join(_HERE, "libmatvec_gpu.so")
 
 MVG_OK = 0
 MVG_E_INVALID = -1

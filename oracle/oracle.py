@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("MVG_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # `make asan` build
 ALGS = {"rowwise": 0, "colwise": 1, "blockwise": 2}
 
 

@@ -38,12 +38,45 @@ def write_inputs(data_dir: str, R: int, C: int, seed_a: int = 42, seed_x: int = 
           "mvg_write_matr_synth")
 
 
+_TOKENS = None
+
+
+def write_synth_rows(path: str, rows: np.ndarray, C: int, seed: int) -> None:
+    """Rows `rows` (global indices, any order) of the synthetic R x C matrix, stacked, as the
+    reference's text (one "%.4f" token per value, README.md:32). Every value is k/10000 with
+    k < 10000, so its text is "0.dddd"; one 7-byte token per value from a table, written
+    band by band (a few hundred MB per second)."""
+    from oracle import oracle
+
+    global _TOKENS
+    if _TOKENS is None:
+        _TOKENS = np.frombuffer(b"".join(b"0.%04d " % k for k in range(10000)), dtype=np.uint8).reshape(10000, 7)
+    rows = np.asarray(rows, dtype=np.int64)
+    # contiguous runs of global rows, each generated at once
+    cuts = np.flatnonzero(np.diff(rows) != 1) + 1
+    step = max(1, (64 << 20) // max(1, 8 * C))
+    with open(path, "wb") as f:
+        for run_rows in np.split(rows, cuts):
+            for b in range(0, len(run_rows), step):
+                r0, nr = int(run_rows[b]), int(min(step, len(run_rows) - b))
+                k = np.rint(oracle.synth_block(r0, nr, 0, C, C, seed) * 10000.0).astype(np.int32)
+                assert k.min() >= 0 and k.max() < 10000
+                txt = _TOKENS[k].reshape(nr, 7 * C)
+                txt[:, -1] = ord("\n")
+                f.write(txt.tobytes())
+
+
 def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str | None = None,
-        cpus: list[int] | None = None) -> dict:
+        cpus: list[int] | None = None, rows: np.ndarray | None = None) -> dict:
     """mpiexec -n P multiplier_<alg> R C in a scratch directory. Returns {"seconds": mean time
     per iteration as the reference printed it, "y": rank 0's y, "wall_s": whole run incl. text
     loading}. With `cpus`, mpiexec and every rank it starts (MPICH's hydra does not bind by
-    default, so ranks inherit the launcher's affinity) run confined to those CPUs.
+    default, so ranks inherit the launcher's affinity) run confined to those CPUs. With `rows`
+    (global row indices of the synthetic R x C matrix), the reference runs on just those rows,
+    stacked into a len(rows) x C matrix: a row's sum depends only on the split of its columns
+    (matr_utils.c:86-96, multiplier_colwise.c:107-122, multiplier_blockwise.c:367), so y is the
+    reference's own y for those rows of the full problem at the same P (whenever the column
+    split is the same: row split, column split, and block split on grids that divide both).
     Raises RuntimeError on any failure."""
     if not available(alg):
         raise RuntimeError(f"reference executable or {MPIEXEC} missing")
@@ -52,7 +85,12 @@ def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str |
     try:
         data = os.path.join(work, "data")
         os.makedirs(os.path.join(data, "out"), exist_ok=True)
-        write_inputs(data, R, C)
+        if rows is None:
+            write_inputs(data, R, C)
+        else:
+            R = len(rows)
+            write_synth_rows(os.path.join(data, f"matrix_{R}_{C}.txt"), rows, C, 42)
+            write_synth_rows(os.path.join(data, f"vector_{C}.txt"), np.zeros(1, dtype=np.int64), C, 4242)
         csv = os.path.join(data, "out", f"{alg}.csv")
         if os.path.exists(csv):
             os.remove(csv)

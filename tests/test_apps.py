@@ -256,3 +256,78 @@ def test_mpiexec_1gib_text_matches_reference(tmp_path, golden, alg, R, C):
     assert "Reading matrix from file" in r.stdout
     name = f"big_{R}x{C}"
     assert max_rel(np.loadtxt(yout), golden[f"{name}/{alg}/P4"]) <= 1e-12
+
+
+# ---- BASELINE.json config 1 as stated: the reference's fixture under `mpirun -np 2`
+# (test.sh:11), every algorithm, through the drop-in executables (both ranks on GPU 0 here)
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("alg", ALGS)
+def test_config1_fixture_mpiexec_two_ranks(workdir, golden, alg, exact):
+    yout = workdir / "y.txt"
+    env = dict(MVG_SAME_DEVICE=1, MVG_ITERS=3, MVG_Y_OUT=yout)
+    if exact:
+        env["MVG_EXACT"] = 1
+    r = mpirun(alg, 2, [4, 8], workdir, **env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "comm_sz = 2\nmy_rank = 0\n" in r.stdout and "launch: 2 ranks" in r.stdout
+    want = golden[f"fixture_4x8/{alg}/P2"]
+    if exact:  # the reference's own y dump, byte for byte
+        assert yout.read_text() == "".join("%.17g\n" % v for v in want)
+    else:
+        assert max_rel(np.loadtxt(yout), want) <= 1e-12
+    lines = (workdir / "data" / "out" / f"{alg}.csv").read_text().splitlines()
+    assert re.fullmatch(r"4, 8, 2, \d+\.\d{6}", lines[1]), lines
+
+
+# ---- eight ranks: the column split's 8 strips and the block split's 2 x 4 grid (config 4's
+# grid, utils.c:26-37; grid-row ncclReduce over 4 ranks, then the leaders' ncclGather through
+# ncclCommSplit), against the real reference's y at P = 8
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,case,R,C,exact", [
+    ("colwise", "sq_480", 480, 480, False), ("colwise", "sq_480", 480, 480, True),
+    ("blockwise", "sq_480", 480, 480, False), ("blockwise", "sq_480", 480, 480, True),
+    ("colwise", "fixture_4x8", 4, 8, True), ("blockwise", "fixture_4x8", 4, 8, True),
+])
+def test_mpiexec_eight_ranks_match_reference(workdir, golden, alg, case, R, C, exact):
+    from oracle import oracle
+
+    yout = workdir / "y.txt"
+    env = dict(MVG_SAME_DEVICE=1, MVG_ITERS=2, MVG_Y_OUT=yout)
+    if case != "fixture_4x8":
+        env["MVG_SYNTH"] = 1
+    if exact:
+        env["MVG_EXACT"] = 1
+    r = mpirun(alg, 8, [R, C], workdir, **env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "launch: 8 ranks" in r.stdout
+    if alg == "blockwise":
+        assert "comm_sz_rows = 2\ncomm_sz_cols = 4\n" in r.stdout
+    want = golden[f"{case}/{alg}/P8"]
+    y = np.loadtxt(yout, ndmin=1)
+    assert max_rel(y, want) <= 1e-12
+    if exact and alg == "colwise":  # MPICH's reduce order, the reference's own y file
+        assert yout.read_text() == "".join("%.17g\n" % v for v in want)
+    elif exact:  # 2 x 4 grid: the reference adds in arrival order; the exact mode in rank order
+        if case == "fixture_4x8":
+            A = np.loadtxt(os.path.join(GOLDEN_DIR, "matrix_4_8.txt")).reshape(4, 8)
+            x = np.loadtxt(os.path.join(GOLDEN_DIR, "vector_8.txt"))
+        else:
+            A, x = oracle.synth(R, C, 42), oracle.synth(1, C, 4242)[0]
+        np.testing.assert_array_equal(y, oracle.multiply(alg, A, x, 8))
+
+
+# ---- the column split at P = 5 and 10 on 720^2: MPICH's reduce-scatter + gather order for a
+# y of more than 2 KiB, where it differs from a binomial tree (oracle/cpu_ref.c ref_mpich_reduce)
+@needs_mpiexec
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [5, 10])
+def test_mpiexec_exact_colwise_mpich_reduce_order(tmp_path, golden, P):
+    (tmp_path / "data" / "out").mkdir(parents=True)
+    yout = tmp_path / "y.txt"
+    r = mpirun("colwise", P, [720, 720], tmp_path, MVG_SYNTH=1, MVG_SAME_DEVICE=1, MVG_EXACT=1, MVG_ITERS=2,
+               MVG_Y_OUT=yout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert yout.read_text() == "".join("%.17g\n" % v for v in golden[f"sq_720/colwise/P{P}"])

@@ -107,3 +107,36 @@ def test_ref_runner_real_reference_matches_oracle():
             np.testing.assert_array_equal(r["y"], want)
         else:
             np.testing.assert_allclose(r["y"], want, rtol=1e-15)
+
+
+# ---- BASELINE configs 2-5 at their own (R, C, P): the reference's y on bands of each config's
+# rows (tests/golden/make_config_slices.py). The oracle on the same rows at the same P must give
+# the reference's bits (block split over > 2 grid columns: its arrival order, 1e-15).
+def _slice_runs():
+    with open(os.path.join(GOLDEN_DIR, "config_slices.json")) as f:
+        meta = json.load(f)
+    return [(c["name"], c["alg"], c["R"], c["C"], int(p[1:])) for c in meta["configs"] for p in c["runs"]]
+
+
+import json  # noqa: E402
+
+
+@pytest.mark.parametrize("cfg,alg,R,C,p", _slice_runs())
+def test_oracle_matches_reference_on_config_rows(cfg, alg, R, C, p):
+    with np.load(os.path.join(GOLDEN_DIR, "config_slices.npz")) as z:
+        rows, want = z[f"{cfg}/rows"], z[f"{cfg}/{alg}/P{p}"]
+    bands = np.split(rows, np.flatnonzero(np.diff(rows) != 1) + 1)
+    A = np.vstack([oracle.synth_block(int(b[0]), len(b), 0, C, C, 42) for b in bands])
+    x = oracle.synth(1, C, 4242)[0]
+    y = oracle.multiply(alg, A, x, p)
+    if alg == "blockwise" and oracle.grid_shape(p)[1] >= 3:
+        assert max_rel(y, want) <= 1e-15
+    else:
+        np.testing.assert_array_equal(y, want)
+
+
+def test_config_slices_cover_every_baseline_config_and_gpu_count():
+    runs = {(cfg, p) for cfg, _, _, _, p in _slice_runs()}
+    assert {("cfg2", 1), ("cfg2", 8), ("cfg5", 8)} <= runs
+    for cfg in ("cfg3", "cfg4"):
+        assert {(cfg, p) for p in (1, 2, 4, 8)} <= runs
