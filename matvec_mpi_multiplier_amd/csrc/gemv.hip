@@ -687,14 +687,12 @@ constexpr int kVecFourRows = variant_id(kVariants, "vec_l64_r4_u4_nt1_o5");
 constexpr int kVecOneRow = variant_id(kVariants, "vec_l64_r1_u4_nt1_o5");
 constexpr int kRowLongOdd = variant_id(kVariants, "rowblk_w4_r2_u8_xcd");
 constexpr int kRowLines = variant_id(kVariants, "rowlines_w8_u4_x0");
-constexpr int kRowLongXcd = kRowLongOdd;  // rowblk_w4_r2_u8_xcd
-constexpr int kRowMidXcd = variant_id(kVariants, "rowblk_w8_r2_u4_xcd");
 constexpr int kVecFourRowsOdd = variant_id(kVariants, "vec_l64_r4_u4_nt1_o0");
 static_assert(kScalarLong > 0 && !kVariants[kScalarLong].vec, "8-B fallback must not need 16-B loads");
 static_assert(kScalarShort > 0 && !kVariants[kScalarShort].vec, "8-B fallback must not need 16-B loads");
 static_assert(kSplitK > 0 && kVariants[kSplitK].split != nullptr, "split-K variant");
 static_assert(kRowLong > 0 && kRowMid > 0 && kRowSmall > 0 && kVecTwoRows > 0 && kVecFourRows > 0 &&
-                  kVecOneRow > 0 && kRowLongOdd > 0 && kVecFourRowsOdd > 0 && kRowLines > 0 && kRowMidXcd > 0,
+                  kVecOneRow > 0 && kRowLongOdd > 0 && kVecFourRowsOdd > 0 && kRowLines > 0,
               "dispatch names a variant missing from kVariants");
 
 constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4 per CU)
@@ -706,24 +704,19 @@ constexpr int64_t kSplitTarget = 1024;  // workgroups a split launch aims for (4
 //   K >= 16384           4 waves x 2 rows x 1024-col chunks (218 VGPR, 8 x 16 B in flight per
 //                        row per lane)
 //   8192 <= K < 16384    8 waves x 2 rows x 512-col chunks
-// Workgroup order (round 2, variant_sweep25_xcd_tall.jsonl, 14 tall shapes x 7 rounds;
-// variant_sweep27_xcd_dispatch.jsonl and variant_sweep28_xcd_recheck.jsonl): the XCD-contiguous
-// order (each XCD streams one row range) wins 0.7-1.8 % from 32768 rows up while the 8 ranges
-// start less than 2 GiB apart (A < 16 GiB: 65536 x 8192 581 -> 573 us, 65536 x 16384 1168 ->
-// 1160, 32768^2 1182 -> 1172, in every run); at 2 GiB apart (65536 x 32768) it won 1.1 % on
-// three allocations and lost 2.7 % on a fourth, so the plain order is kept there; from 4 GiB
-// apart (65536^2, 131072^2) it loses 5-7 % (the 8 streams on the same HBM channels); at 16384^2
-// it is 0.5 % behind.
+// Workgroup order: the plain one. The XCD-contiguous order (each XCD streams one row range) won
+// only 0.7-1.8 % on aligned tall shapes with the 8 ranges < 2 GiB apart (round 2,
+// variant_sweep25/27/28_*.jsonl), flipped sign across allocations at 2 GiB apart and lost 5-7 %
+// from 4 GiB apart: inside the +-5 % box-to-box spread, so round 3 dropped it for aligned rows.
 // Shorter rows (768 < K < 8192), by the size of A (variant_sweep14_grid.jsonl: 42 shapes
 // 1024..65536 x 1024..12288, the reference's test.sh squares among them):
 //   A < 1 GiB         row-per-workgroup again: 2 waves x 2 rows x 512-col chunks, or 8 waves for
 //                     6144 <= K with >= 700 workgroups (within 1.024x of the best variant on
 //                     average over those shapes, worst 1.08x; the wave-owns-rows forms below
 //                     were up to 1.57x slower there: 4200^2 29 -> 23.6 us, 1800^2 7.3 -> 5.5 us)
-//   A >= 1 GiB, 3072 <= K   the long-row form in XCD order where the rule above allows it,
-//                     else 8 waves x 2 rows for K >= 4096 (variant_sweep26_midk_tall.jsonl, 13
-//                     shapes: 131072 x 6144 906 -> 862 us, 131072 x 3072 446 -> 438, 524288 x
-//                     4096 2373 -> 2314 plain; at K = 2048 the wave-owns-rows form stays 6 % ahead)
+//   A >= 1 GiB, 4096 <= K   8 waves x 2 rows (variant_sweep26_midk_tall.jsonl, 13 shapes:
+//                     131072 x 6144 906 -> 862 us, 524288 x 4096 2373 -> 2314; at K = 2048 the
+//                     wave-owns-rows form stays 6 % ahead)
 //   A >= 1 GiB, 1536 < K    wave-owns-2-rows, pipelined + staggered start column
 //   A >= 1 GiB, K <= 1536   wave-owns-4-rows, pipelined
 //   K <= 768          one row per wave (the whole row is one chunk: 524288 short waves stream
@@ -750,14 +743,12 @@ static int pick_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool al
         return K > 768 ? kRowSmall : kVecFourRowsOdd;
     }
     const int64_t nrb = (M + 1) / 2;
-    const bool xcd = M >= 32768 && M * lda < (int64_t)(1ll << 31);  // XCD ranges < 2 GiB apart
     if (K >= 8192) {
         if (nrb < 700) return kSplitK;
-        if (xcd) return K >= 16384 ? kRowLongXcd : kRowMidXcd;
         return K >= 16384 ? kRowLong : kRowMid;
     }
     if (K > 768 && M * K < (int64_t)(1ll << 27)) return K >= 6144 && nrb >= 700 ? kRowMid : kRowSmall;
-    if (K >= 3072 && (xcd || K >= 4096)) return xcd ? kRowLongXcd : kRowMid;
+    if (K >= 4096) return kRowMid;
     if (K > 1536) return kVecTwoRows;
     if (K > 768) return kVecFourRows;
     return kVecOneRow;

@@ -342,7 +342,7 @@ def test_auto_variant_names_match_the_dispatch_table():
              for m, k in ((16384, 16384), (65536, 32768), (65536, 8192), (524288, 4096), (2097152, 1024),
                           (4194304, 512))}
     assert names[16384] == "rowblk_w4_r2_u8" and names[32768] == "rowblk_w4_r2_u8"
-    assert names[8192] == "rowblk_w8_r2_u4_xcd" and names[512] == "vec_l64_r1_u4_nt1_o5"
+    assert names[8192] == "rowblk_w8_r2_u4" and names[512] == "vec_l64_r1_u4_nt1_o5"
     pick = lambda m, k: _lib.lib.mvg_gemv_variant_name(_lib.lib.mvg_gemv_auto_variant(k, m, k)).decode()
     assert pick(120, 60000) == "rowblk_w4_r2_u4_splitk" and pick(1024, 131072) == "rowblk_w4_r2_u4_splitk"
     assert pick(4096, 16384) == "rowblk_w4_r2_u8" and pick(1536, 32768) == "rowblk_w4_r2_u8"
@@ -353,13 +353,14 @@ def test_auto_variant_names_match_the_dispatch_table():
     assert pick(7800, 7800) == "rowlines_w8_u4_x0" and pick(10200, 10200) == "rowlines_w8_u4_x0"
     assert pick(16384, 16386) == "rowlines_w8_u4_x0" and pick(16384, 16400) == "rowblk_w4_r2_u8"
     assert names[4096] == "rowblk_w8_r2_u4" and names[1024] == "vec_l64_r4_u4_nt1_o5"
-    # XCD-contiguous order only from 32768 rows and while the 8 row ranges are < 2 GiB apart
+    # aligned rows keep the plain workgroup order (the XCD-contiguous one gained < 2 %)
     assert pick(65536, 65536) == "rowblk_w4_r2_u8" and pick(131072, 131072) == "rowblk_w4_r2_u8"
-    assert pick(131072, 32768) == "rowblk_w4_r2_u8" and pick(131072, 16384) == "rowblk_w4_r2_u8" and pick(65536, 16384) == "rowblk_w4_r2_u8_xcd"
-    assert pick(32768, 8192) == "rowblk_w8_r2_u4_xcd" and pick(16384, 8192) == "rowblk_w8_r2_u4"
-    # A >= 1 GiB, 3072 <= K < 8192: row-block forms; K = 2048 keeps the wave-owns-rows form
-    assert pick(131072, 3072) == "rowblk_w4_r2_u8_xcd" and pick(1048576, 2048) == "vec_l64_r2_u4_nt1_o7"
-    assert pick(65536, 4200) == "rowblk_w4_r2_u8_xcd" and pick(8388608, 4096) == "rowblk_w8_r2_u4"
+    assert pick(131072, 32768) == "rowblk_w4_r2_u8" and pick(131072, 16384) == "rowblk_w4_r2_u8"
+    assert pick(65536, 16384) == "rowblk_w4_r2_u8"
+    assert pick(32768, 8192) == "rowblk_w8_r2_u4" and pick(16384, 8192) == "rowblk_w8_r2_u4"
+    # A >= 1 GiB, 4096 <= K < 8192: the row-block form; K <= 3072 keeps the wave-owns-rows form
+    assert pick(131072, 3072) == "vec_l64_r2_u4_nt1_o7" and pick(1048576, 2048) == "vec_l64_r2_u4_nt1_o7"
+    assert pick(65536, 4200) == "rowblk_w8_r2_u4" and pick(8388608, 4096) == "rowblk_w8_r2_u4"
     assert pick(8388608, 3072) == "vec_l64_r2_u4_nt1_o7"
     # odd widths (odd lda): the 16-B kernels through unaligned loads, not the 8-B ones
     assert pick(16384, 16383) == "rowlines_w8_u4_x0" and pick(65536, 8191) == "rowlines_w8_u4_x0"
