@@ -514,13 +514,15 @@ def rccl_report(path, distributed, rank):
 
     import torch.distributed as dist
 
-    mine = {"links": {}, "nranks": []}
+    mine = {"links": {}, "nranks": [], "samples": []}
     if path and os.path.exists(path):
         pat = re.compile(r"(\d+)\[\d+\] -> (\d+)\[\d+\](?: \[(?:send|receive)\])? via (\S+)")
         for line in open(path, errors="replace"):
             m = pat.search(line)
             if m:
                 mine["links"].setdefault(f"{m.group(1)}->{m.group(2)}", set()).add(m.group(3))
+                if len(mine["samples"]) < 2:
+                    mine["samples"].append(line.strip()[-160:])
             m = re.search(r"nranks (\d+)", line)
             if m and "Init COMPLETE" in line:
                 mine["nranks"].append(int(m.group(1)))
@@ -535,16 +537,17 @@ def rccl_report(path, distributed, rank):
         return None
     if path is None:
         return {"logged": False, "why": "NCCL_DEBUG set by the caller"}
-    links, counts, sizes = {}, {}, set()
+    links, counts, sizes, samples = {}, {}, set(), []
     for r in allr:
         sizes.update(r["nranks"])
+        samples += r["samples"][: max(0, 4 - len(samples))]
         for k, v in r["links"].items():
             links.setdefault(k, set()).update(v)
     for v in links.values():
         for t in v:
             counts[t] = counts.get(t, 0) + 1
     return {"logged": True, "comm_sizes": sorted(sizes), "transport_counts": counts,
-            "links": {k: sorted(v) for k, v in sorted(links.items())}}
+            "links": {k: sorted(v) for k, v in sorted(links.items())}, "log_samples": samples}
 
 
 def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_bytes, local):

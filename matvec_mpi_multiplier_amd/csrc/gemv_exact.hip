@@ -321,6 +321,11 @@ __device__ __forceinline__ double hop_masked_segment(double sum, const double* _
     return fwd ? hop_segment<L, W, true>(sum, ta, tx) : hop_segment<L, W, false>(sum, ta, tx);
 }
 
+// every row of A starts on a 128-B line: A on a line and lda a multiple of 16 doubles
+__device__ __forceinline__ bool lines_aligned(const double* A, int64_t lda) {
+    return (((uintptr_t)A & 127u) == 0) && (lda % 16 == 0);
+}
+
 // Segment g of a row runs forward (lane 0 -> L-1) when g is even. A row's segments: a head
 // (g = 0) ending at the row's first 128-B boundary, so that every main segment's loads start on
 // a cache line — a row that starts mid-line would make each 128-B piece touch two lines
@@ -349,7 +354,11 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
         // head: columns [0, h) with h the distance to the row's next 128-B boundary (0 ... 15)
         const int64_t h = (int64_t)(((128u - ((uintptr_t)arow & 127u)) & 127u) >> 3);
         sum = hop_masked_segment<L, W>(sum, arow, x, h - S + off[0], 0, h < K ? h : K, true);
-        nseg = K >= 15 ? (K - 15) / S : 0;            // every row has >= nseg * S columns past its head
+        // every row has >= nseg * S columns past its head; when every row starts on a line (A on
+        // a line, lda a multiple of 16: h = 0 throughout) that is K / S, and a row of whole
+        // segments (config 5's 512 columns) needs no masked tail, whose loads would not be in
+        // flight ahead of the chain
+        nseg = lines_aligned(A, lda) ? K / S : K >= 15 ? (K - 15) / S : 0;
         ntail = (K - nseg * S + S - 1) / S;            // the most any row has left: 1 or 2 segments
         const double* ar = arow + h;
         const double* xr = x + h;
@@ -366,8 +375,10 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
             // segments ahead; the scheduling barriers keep the loads in slot order, so the
             // compiler's vmcnt waits retire exactly the slot about to be summed. Main segment i
             // is the row's segment i + 1 (after the head).
+            // (strict <: a group whose refills would all lie past the row's last segment is left
+            // to the remainder below instead of re-reading that segment U times)
             int64_t base = 0;
-            for (; base + U <= nseg; base += U) {
+            for (; base + U < nseg; base += U) {
 #pragma unroll
                 for (int i = 0; i < U; ++i) {
                     sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
@@ -378,7 +389,7 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
-            // the last nseg % U segments are already in slots 0 .. nseg % U - 1 (base is even)
+            // the last nseg - base <= U segments are already in slots 0 .. nseg - base - 1 (base is even)
 #pragma unroll
             for (int i = 0; i < U; ++i)
                 if (base + i < nseg)
@@ -393,6 +404,78 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
     const int holder = (K > 0 && ((1 + nseg + ntail) & 1)) ? L - 1 : 0;
     if (c == holder && row < M) y[row] = sum;
 }
+
+// gemv_seq_hop with x staged in LDS once per workgroup of NW waves (short rows, K <= kXlMaxK):
+// the main segments read their x pieces from LDS (all row groups of a wave read the same 16 B per
+// lane group: broadcasts) instead of re-reading x through L1 beside the A stream, so the vector
+// memory pipeline carries A alone. Same chain, same order, same bits as gemv_seq_hop<L, W, U, true>.
+template <int L, int W, int U, int NW>
+__global__ __launch_bounds__(64 * NW) void gemv_seq_hop_xl(const double* __restrict__ A, int64_t lda,
+                                                           const double* __restrict__ x,
+                                                           double* __restrict__ y, int64_t M, int64_t K) {
+    static_assert(L == 4 || L == 8 || L == 16, "lanes per row");
+    static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B pieces; segment pairs per unrolled step");
+    extern __shared__ double xl[];  // K doubles
+    constexpr int R = 64 / L;
+    constexpr int S = L * W;
+    constexpr int V = W / 2;
+    static_assert(S >= 16, "the head (up to 15 columns) fits one segment");
+    for (int64_t j = threadIdx.x; j < K; j += 64 * NW) xl[j] = x[j];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int c = lane % L;
+    const int64_t row = ((int64_t)blockIdx.x * NW + (threadIdx.x >> 6)) * R + lane / L;
+    const int64_t rr = row < M ? row : M - 1;
+    const double* arow = A + rr * lda;
+    const int off[2] = {c * W, (L - 1 - c) * W};
+    double sum = 0.0;
+    int64_t nseg = 0, ntail = 0;
+    if (K > 0) {
+        const int64_t h = (int64_t)(((128u - ((uintptr_t)arow & 127u)) & 127u) >> 3);
+        sum = hop_masked_segment<L, W>(sum, arow, x, h - S + off[0], 0, h < K ? h : K, true);
+        nseg = lines_aligned(A, lda) ? K / S : K >= 15 ? (K - 15) / S : 0;
+        ntail = (K - nseg * S + S - 1) / S;
+        const double* ar = arow + h;
+        const double* xr = xl + h;
+        auto xload = [&](const double* p, dbl2x (&d)[V]) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) d[v] = dbl2x{p[2 * v], p[2 * v + 1]};
+        };
+        if (nseg > 0) {
+            dbl2x a[U][V], xv[U][V];
+#pragma unroll
+            for (int i = 0; i < U; ++i) {
+                const int64_t sg = i < nseg ? i : nseg - 1;
+                load_run<V, true, true>(ar + sg * S + off[(i + 1) & 1], a[i]);
+                xload(xr + sg * S + off[(i + 1) & 1], xv[i]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            int64_t base = 0;
+            for (; base + U < nseg; base += U) {
+#pragma unroll
+                for (int i = 0; i < U; ++i) {
+                    sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int64_t sg = base + i + U < nseg ? base + i + U : nseg - 1;
+                    load_run<V, true, true>(ar + sg * S + off[(i + 1) & 1], a[i]);
+                    xload(xr + sg * S + off[(i + 1) & 1], xv[i]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < U; ++i)
+                if (base + i < nseg)
+                    sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
+        }
+        for (int64_t t = 0; t < ntail; ++t) {
+            const int64_t g = 1 + nseg + t;
+            sum = hop_masked_segment<L, W>(sum, arow, x, h + (nseg + t) * S + off[g & 1], h, K, (g & 1) == 0);
+        }
+    }
+    const int holder = (K > 0 && ((1 + nseg + ntail) & 1)) ? L - 1 : 0;
+    if (c == holder && row < M) y[row] = sum;
+}
+constexpr int64_t kXlMaxK = 8192;  // x in LDS: up to 64 KiB per workgroup
 
 // ------------------------------------------------------------------ column-panel layout
 // Every exact form streams all M rows at once — a row's chain (>= 2.5 ns per column) is too slow
@@ -442,7 +525,7 @@ __global__ __launch_bounds__(64) void gemv_seq_hop_panel(const double* __restric
         // slot order so the counted vmcnt waits retire exactly the slot about to be summed;
         // segment g runs forward when g is even (base is a multiple of U, U even)
         int64_t base = 0;
-        for (; base + U <= nseg; base += U) {
+        for (; base + U < nseg; base += U) {
 #pragma unroll
             for (int i = 0; i < U; ++i) {
                 sum = (i & 1) ? hop_segment<L, W, false>(sum, a[i], xv[i]) : hop_segment<L, W, true>(sum, a[i], xv[i]);
@@ -586,7 +669,9 @@ struct SeqVariant {
     const char* name;
     seq_fn fn;
     int needs;  // operand requirements: kAnyOperands, kVec16 or kVec16Lda23 (below)
-    int rows;  // rows per one-wave workgroup
+    int rows;   // rows per workgroup
+    int waves = 1;       // waves per workgroup
+    bool xlds = false;   // x staged in LDS (K doubles of dynamic LDS; K <= kXlMaxK)
 };
 
 // kVec16: 16-B loads, so 16-B aligned A and x and an even lda; kVec16Lda23: also 32-bit
@@ -595,6 +680,8 @@ constexpr int kAnyOperands = 0, kVec16 = 1, kVec16Lda23 = 2;
 #define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, kVec16Lda23, RW}
 #define HOP(L, W, U) {"hop_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U>, kVec16, 64 / L}
 #define HOP8(L, W, U) {"hop8_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U, true>, kAnyOperands, 64 / L}
+#define HOPXL(L, W, U, NW) \
+    {"hopxl_l" #L "_w" #W "_u" #U "_n" #NW, gemv_seq_hop_xl<L, W, U, NW>, kAnyOperands, NW * 64 / L, NW, true}
 static constexpr SeqVariant kSeqVariants[] = {
     {"auto", nullptr, kAnyOperands, 64},  // 0
     {"seq_scalar", gemv_seq_scalar, kAnyOperands, 64},
@@ -631,6 +718,11 @@ static constexpr SeqVariant kSeqVariants[] = {
     HOP8(16, 4, 8),
     HOP8(16, 8, 4),
     HOP8(32, 8, 4),
+    // x staged in LDS once per workgroup of NW waves (short rows)
+    HOPXL(8, 2, 16, 4),
+    HOPXL(8, 2, 8, 4),
+    HOPXL(4, 4, 8, 4),
+    HOPXL(8, 2, 16, 2),
 };
 constexpr int kNumSeqVariants = (int)(sizeof(kSeqVariants) / sizeof(kSeqVariants[0]));
 
@@ -750,13 +842,16 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         return fail(MVG_E_INVALID, kSeqVariants[v].needs == kVec16
                                        ? "mvg_gemv_exact: 16-B variant needs 16-B aligned A, x and an even lda"
                                        : "mvg_gemv_exact: LDS-DMA variant needs 16-B aligned A, x and an even lda < 2^23");
+    const SeqVariant& var = kSeqVariants[v];
+    if (var.xlds && k > kXlMaxK) return fail(MVG_E_INVALID, "mvg_gemv_exact: x-in-LDS variant needs k <= 8192");
     // k == 0 runs the kernel too: every row's sum stays 0 (the reference's `sum = 0`)
     // grid-size cap: fewer than 2^32 threads per launch
-    const int64_t max_rows = ((1ll << 26) - 1) * kSeqVariants[v].rows;
+    const int64_t max_rows = ((1ll << 32) / (64 * var.waves) - 1) * var.rows;
+    const size_t lds = var.xlds ? (size_t)k * sizeof(double) : 0;
     for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
         const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
-        const int rw = kSeqVariants[v].rows;
-        hipLaunchKernelGGL(kSeqVariants[v].fn, dim3((unsigned)((mm + rw - 1) / rw)), dim3(64), 0, s,
+        const int rw = var.rows;
+        hipLaunchKernelGGL(var.fn, dim3((unsigned)((mm + rw - 1) / rw)), dim3(64 * var.waves), lds, s,
                            A ? A + r0 * lda : A, lda, x, y + r0, mm, k);
         MVG_HIP(hipGetLastError());
     }

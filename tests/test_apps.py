@@ -235,6 +235,13 @@ def test_bench_two_ranks_one_device(tmp_path):
     assert cfg["config 3"]["shard"] == [65536, 32768] and cfg["config 3"]["value"] > 0
     assert cfg["config 4"]["grid"] == [1, 2] and cfg["config 4"]["shard"] == [131072, 65536]
     assert cfg["config 5"]["shard"] == [2097152, 512] and cfg["config 5"]["value"] > 0
+    # every config's y against the real reference's own rows at P = 2 (tests/golden/config_slices.npz)
+    for name in ("config 3", "config 4"):
+        ref = cfg[name]["reference_rows"]
+        assert ref["P"] == 2 and ref["rows"] == 512 and ref["max_rel"] <= 1e-12, ref
+        assert ref["exact_bit_identical"], ref  # grids of <= 2 columns: deterministic reference sums
+    # the transports RCCL reported for its connections (loopback sockets here: both ranks on GPU 0)
+    assert d["rccl"]["logged"] and 2 in d["rccl"]["comm_sizes"] and d["rccl"]["transport_counts"], d["rccl"]
 
 
 # ---- the drop-in contract at 1 GiB: the reference's text format written for a 16384 x 8192

@@ -39,6 +39,11 @@ def needs_16b(name):
     return name.startswith(("seq_r", "seqx_", "hop_"))
 
 
+def xl_k_limited(name):
+    """`hopxl_*` stage all of x in LDS: k <= 8192 (64 KiB), refused above."""
+    return name.startswith("hopxl_")
+
+
 def exact_variants():
     lib = _lib.lib
     return [(v, lib.mvg_gemv_exact_variant_name(v).decode()) for v in range(lib.mvg_gemv_exact_variant_count())]
@@ -50,7 +55,7 @@ def test_gemv_exact_every_variant_is_the_reference_sum(m, k):
     x = signed(oracle.synth(1, k, 4242)[0], k)
     want = oracle.multiply_std_rowwise(A, x)
     for v, name in exact_variants():
-        if needs_16b(name) and k % 2:  # the 16-B forms need an even lda
+        if (needs_16b(name) and k % 2) or (xl_k_limited(name) and k > 8192):  # forms that refuse the shape
             with pytest.raises(_lib.MvgError):
                 mm.multiply_std_rowwise(A, x, variant=v, exact=True)
             continue
@@ -68,8 +73,9 @@ def test_gemv_exact_hop_segment_edges():
         if not name.startswith("hop"):
             continue
         L, W, U = (int(part[1:]) for part in name.split("_")[1:4])
+        nw = int(name.split("_n")[-1]) if xl_k_limited(name) else 1  # waves per workgroup
         S = L * W
-        m = 3 * (64 // L) + 1
+        m = 3 * nw * (64 // L) + 1
         ks = [S - 2, S, 3 * S + 2, (U + 1) * S, (U + 1) * S + 2, (U + 2) * S, 2 * U * S, 2 * U * S + 2,
               (3 * U - 1) * S]
         if not needs_16b(name):  # odd widths too: every other row starts 8 bytes off a 16-B boundary
@@ -208,14 +214,8 @@ def test_engine_exact_shard_products_and_combines_at_p_gt_1(golden, manifest):
             parts.append(mm.multiply_std_rowwise(blk, x[sh.col_off:sh.col_off + sh.n_cols], exact=True))
         if alg == "rowwise":
             y = np.concatenate(parts)
-        elif alg == "colwise":
-            bufs = [q.copy() for q in parts]
-            mask = 1
-            while mask < p:
-                for r in range(0, p - mask, 2 * mask):
-                    bufs[r] = bufs[r] + bufs[r + mask]
-                mask *= 2
-            y = bufs[0]
+        elif alg == "colwise":  # MPICH's MPI_Reduce order (the engine's combine_mpich)
+            y = oracle.mpich_reduce(parts)
         else:
             gr, gc = mm.get_2_most_closest_multipliers(p)
             y = np.zeros(R)
