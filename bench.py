@@ -69,8 +69,8 @@ def parse():
     ap.add_argument("--config-steps", type=int, default=20)
     ap.add_argument("--no-config-cpu-baseline", action="store_true",
                     help="skip the per-config CPU baselines (configs 3-5, N = 1)")
-    ap.add_argument("--config-ref-rows", type=int, default=128,
-                    help="rows of each config's slice the real reference runs on")
+    ap.add_argument("--config-ref-bytes", type=float, default=64 * 2 ** 20,
+                    help="size of the leading-row slice the real reference runs on per config (>= 128 rows)")
     ap.add_argument("--config-cpu-sample-bytes", type=float, default=3.5e10,
                     help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
     ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
@@ -460,7 +460,8 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 # the reference on a leading-row slice at the host's core count, and the -O2 port
                 # on the whole config where host memory allows (config 4: its leading rows)
                 try:
-                    entry["cpu_baseline"] = cpu_baseline(args, alg, R, C, y, None, ref_rows=args.config_ref_rows,
+                    ref_rows = min(R, max(128, int(args.config_ref_bytes // (8 * C))))
+                    entry["cpu_baseline"] = cpu_baseline(args, alg, R, C, y, None, ref_rows=ref_rows,
                                                          sample_bytes=args.config_cpu_sample_bytes,
                                                          cpu_seconds=args.config_cpu_seconds, placements=("spread",))
                 except Exception as exc:  # the baseline must never sink the bench
