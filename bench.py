@@ -506,32 +506,42 @@ def mm_grid_cols(n):
     return mm.get_2_most_closest_multipliers(n)[1]
 
 
+def parse_rccl_log(lines):
+    """RCCL's NCCL_DEBUG=INFO lines -> {"links": {"a->b": [transport, ...]}, "nranks": [...],
+    "samples": [...]}: the transport of every connection it set up ("Channel 00/0 : 0[0] -> 1[1]
+    via P2P/IPC", "... [send] via NET/Socket/0") and the size of every communicator it reports
+    initialised ("... nranks 8 ... Init COMPLETE")."""
+    import re
+
+    pat = re.compile(r"(\d+)\[\w+\] -> (\d+)\[\w+\](?: \[(?:send|receive)\])? via (\S+)")
+    links, nranks, samples = {}, [], []
+    for line in lines:
+        m = pat.search(line)
+        if m:
+            links.setdefault(f"{m.group(1)}->{m.group(2)}", set()).add(m.group(3))
+            if len(samples) < 2:
+                samples.append(line.strip()[-160:])
+        m = re.search(r"nranks (\d+)", line)
+        if m and "Init COMPLETE" in line:
+            nranks.append(int(m.group(1)))
+    return {"links": {k: sorted(v) for k, v in links.items()}, "nranks": nranks, "samples": samples}
+
+
 def rccl_report(path, distributed, rank):
     """What RCCL reported about its communicators, all ranks gathered on rank 0: the transport of
     every connection it set up ("a->b": P2P/IPC, P2P/direct pointer, SHM, NET/...), counted per
     transport, and the communicator sizes (nranks) it initialised. Parsed from the NCCL_DEBUG=INFO
     file each rank wrote (NCCL_DEBUG_FILE); None when the caller set NCCL_DEBUG itself."""
-    import re
-
     import torch.distributed as dist
 
     mine = {"links": {}, "nranks": [], "samples": []}
     if path and os.path.exists(path):
-        pat = re.compile(r"(\d+)\[\d+\] -> (\d+)\[\d+\](?: \[(?:send|receive)\])? via (\S+)")
-        for line in open(path, errors="replace"):
-            m = pat.search(line)
-            if m:
-                mine["links"].setdefault(f"{m.group(1)}->{m.group(2)}", set()).add(m.group(3))
-                if len(mine["samples"]) < 2:
-                    mine["samples"].append(line.strip()[-160:])
-            m = re.search(r"nranks (\d+)", line)
-            if m and "Init COMPLETE" in line:
-                mine["nranks"].append(int(m.group(1)))
+        with open(path, errors="replace") as f:
+            mine = parse_rccl_log(f)
         try:
             os.remove(path)
         except OSError:
             pass
-    mine["links"] = {k: sorted(v) for k, v in mine["links"].items()}
     allr = [None] * dist.get_world_size()
     dist.all_gather_object(allr, mine)
     if rank != 0:

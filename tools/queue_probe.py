@@ -1,11 +1,13 @@
-"""Does anything else the process sets up slow the exact GEMV down? (development tool, one MI355X)
+"""Does the number of HIP streams (hardware queues) a process holds slow the exact GEMV down?
+(development tool, one MI355X)
 
     python tools/queue_probe.py [M] [K] [launches]
 
-Times mvg_gemv (tree) and mvg_gemv_exact on one torch-allocated A, on torch's current stream, at
-each stage of a process's life: alone; after an RCCL communicator (mm.Comm.init_all); after an
-engine on it (mm.Multiplier: its own streams and buffers); after more HIP streams; after the
-engine and the communicator are destroyed. One JSON object per stage.
+Times mvg_gemv (tree) and mvg_gemv_exact on one torch-allocated A, on torch's current stream,
+as the process adds HIP streams: none; 1, 2, 3 and 6 more streams that each ran one tiny kernel
+(the HIP runtime maps streams onto at most GPU_MAX_HW_QUEUES = 4 hardware queues per process);
+then an RCCL communicator and a small engine (its own streams) on top. Three timings per stage,
+the stages repeated in reverse at the end. One JSON object per stage.
 """
 import json
 import os
@@ -41,30 +43,36 @@ def main():
         return round(e0.elapsed_time(e1) / n * 1e3, 2)
 
     def stage(name):
-        out = {"stage": name}
-        for _ in range(2):
-            out.setdefault("tree_us", []).append(t(lambda: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)))
-            out.setdefault("exact_us", []).append(
-                t(lambda: lib.mvg_gemv_exact(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)))
+        out = {"stage": name, "tree_us": [], "exact_us": []}
+        for _ in range(3):
+            out["tree_us"].append(t(lambda: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)))
+            out["exact_us"].append(t(lambda: lib.mvg_gemv_exact(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)))
         print(json.dumps(out), flush=True)
 
-    stage("alone")
+    streams = []
+
+    def add_streams(k):
+        for _ in range(k):
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                torch.zeros(1, device="cuda:0").add_(1)
+            streams.append(st)
+        torch.cuda.synchronize()
+
+    stage("no extra stream")
+    for k, total in ((1, 1), (1, 2), (1, 3), (3, 6)):
+        add_streams(k)
+        stage(f"{total} extra used stream(s)")
     comm = mm.Comm.init_all([0])
-    stage("after RCCL communicator (init_all)")
+    stage("+ RCCL communicator")
     eng = mm.Multiplier("rowwise", 2048, 2048, comm)
     eng.fill_synth()
     eng.multiply()
     eng.sync()
-    stage("after a small engine (its streams, one multiply)")
-    extra = [torch.cuda.Stream() for _ in range(6)]
-    for st in extra:
-        with torch.cuda.stream(st):
-            torch.zeros(1, device="cuda:0").add_(1)
-    torch.cuda.synchronize()
-    stage("after 6 more used torch streams")
+    stage("+ engine (its streams, one multiply)")
     eng.destroy()
     comm.destroy()
-    stage("after engine and communicator destroyed")
+    stage("engine and communicator destroyed")
 
 
 if __name__ == "__main__":
