@@ -384,7 +384,7 @@ def test_exact_panel_dispatch_and_argument_checks():
     assert width(6144, 2048) == 0                # under 128 MiB
     assert width(4096, 65536) == 0 and width(4194304, 512) == 0  # few rows / short rows
     name = lambda m, k: lib.mvg_gemv_exact_panel_variant_name(lib.mvg_gemv_exact_panel_auto_variant(m, k)).decode()  # noqa: E731
-    assert name(16384, 16384) == "panel_l8_w2_u8" and name(65536, 8192) == "panel_l8_w2_u24"
+    assert name(16384, 16384) == "panel_l8_w2_u8" and name(65536, 8192) == "panel_l8_w2_u8"
     names = [lib.mvg_gemv_exact_panel_variant_name(v).decode() for v in range(lib.mvg_gemv_exact_panel_variant_count())]
     assert names[0] == "auto" and all(n.startswith("panel_l") for n in names[1:])
     assert lib.mvg_gemv_exact_panel_variant_name(len(names)) == b"invalid"
