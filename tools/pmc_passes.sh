@@ -9,6 +9,7 @@ set -euo pipefail
 OUT="$1"; M="$2"; K="$3"; shift 3
 PASSES=(
   "fetch:FETCH_SIZE"
+  "write:WRITE_SIZE"
   "l2:TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"
   "ta:TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE"
   "sq:SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE"
