@@ -108,8 +108,10 @@ def main():
     # the HIP runtime starts. With N > 1, RCCL logs its transport choices to a per-rank file that
     # rccl_report() reads back (P2P/IPC over xGMI, or SHM / NET), unless the caller set NCCL_DEBUG.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    rccl_log = None
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG" not in os.environ:
+    # (INFO goes to the file only, so a caller's quieter NCCL_DEBUG level on stderr is unaffected;
+    # a caller who directs RCCL's log to a file of their own keeps it, and the report is skipped)
+    rccl_log, caller_debug = None, os.environ.get("NCCL_DEBUG")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG_FILE" not in os.environ:
         rccl_log = f"/tmp/mvg_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log"
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=rccl_log)
     import torch
@@ -219,6 +221,8 @@ def main():
             exact["bit_identical_to_reference_sample"] = same_ref
 
     rccl = rccl_report(rccl_log, distributed, rank) if distributed else None
+    if rccl is not None:
+        rccl["caller_NCCL_DEBUG"] = caller_debug
     ref_rows = None
     if rank == 0 and args.alg == "rowwise" and (R, C) == (SHARD, SHARD):
         ref_rows = reference_rows_check("config 2", "rowwise", R, C, n, y, y_exact)
@@ -547,7 +551,7 @@ def rccl_report(path, distributed, rank):
     if rank != 0:
         return None
     if path is None:
-        return {"logged": False, "why": "NCCL_DEBUG set by the caller"}
+        return {"logged": False, "why": "NCCL_DEBUG_FILE set by the caller"}
     links, counts, sizes, samples = {}, {}, set(), []
     for r in allr:
         sizes.update(r["nranks"])

@@ -272,22 +272,17 @@ __device__ __forceinline__ double hop(double v) {
 }
 
 // One segment of the chain: lane t of the group adds its W products at step t, then hands over.
-// MA (masked adds): only the lane holding the chain executes its adds (the others are switched
-// off in the exec mask instead of adding into a value the next hop overwrites) — the same bits,
-// an eighth of the VALU work at L = 8 (a power experiment: the issue cycles stay the same).
-template <int L, int W, bool FWD, bool MA = false>
+// Every lane executes every add (switching the non-holders off in the exec mask, an eighth of the
+// VALU work at L = 8, measured no faster: round 3, profiles/r03/sweep_exact_masked.jsonl).
+template <int L, int W, bool FWD>
 __device__ __forceinline__ double hop_segment(double sum, const dbl2x (&a)[W / 2], const dbl2x (&xv)[W / 2]) {
     double p[W];
 #pragma unroll
     for (int v = 0; v < W / 2; ++v) p[2 * v] = a[v].x * xv[v].x, p[2 * v + 1] = a[v].y * xv[v].y;
-    const int c = (int)(threadIdx.x & 63) % L;
-    const int me = FWD ? c : L - 1 - c;  // the step at which this lane holds the chain
 #pragma unroll
     for (int t = 0; t < L; ++t) {
-        if (!MA || me == t) {
 #pragma unroll
-            for (int j = 0; j < W; ++j) sum = sum + p[j];
-        }
+        for (int j = 0; j < W; ++j) sum = sum + p[j];
         if (t + 1 < L) sum = hop<L, FWD>(sum);
     }
     return sum;
@@ -339,7 +334,7 @@ __device__ __forceinline__ bool lines_aligned(const double* A, int64_t lda) {
 // (16384 x 16386: 373 us against 314 us at 16384^2, sweep_exact13_lines.jsonl) — then nseg
 // main segments, the same count for every row of the wave, then one or two tail segments for
 // what is left. Head and tails are masked segments (zeros outside the row's columns).
-template <int L, int W, int U, bool B8 = false, bool MA = false>
+template <int L, int W, int U, bool B8 = false>
 __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ x,
                                                    double* __restrict__ y, int64_t M, int64_t K) {
@@ -388,7 +383,7 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
             for (; base + U < nseg; base += U) {
 #pragma unroll
                 for (int i = 0; i < U; ++i) {
-                    sum = (i & 1) ? hop_segment<L, W, true, MA>(sum, a[i], xv[i]) : hop_segment<L, W, false, MA>(sum, a[i], xv[i]);
+                    sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
                     __builtin_amdgcn_sched_barrier(0);
                     const int64_t sg = base + i + U < nseg ? base + i + U : nseg - 1;
                     load_run<V, B8, true>(ar + sg * S + off[(i + 1) & 1], a[i]);
@@ -400,7 +395,7 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
 #pragma unroll
             for (int i = 0; i < U; ++i)
                 if (base + i < nseg)
-                    sum = (i & 1) ? hop_segment<L, W, true, MA>(sum, a[i], xv[i]) : hop_segment<L, W, false, MA>(sum, a[i], xv[i]);
+                    sum = (i & 1) ? hop_segment<L, W, true>(sum, a[i], xv[i]) : hop_segment<L, W, false>(sum, a[i], xv[i]);
         }
         for (int64_t t = 0; t < ntail; ++t) {
             const int64_t g = 1 + nseg + t;  // the row's segment index
@@ -725,9 +720,6 @@ static constexpr SeqVariant kSeqVariants[] = {
     HOP8(16, 4, 8),
     HOP8(16, 8, 4),
     HOP8(32, 8, 4),
-    // only the chain's holder adds (exec-masked; same bits, a power experiment)
-    {"hop8m_l8_w2_u16", gemv_seq_hop<8, 2, 16, true, true>, kAnyOperands, 8},
-    {"hop8m_l8_w2_u24", gemv_seq_hop<8, 2, 24, true, true>, kAnyOperands, 8},
     // x staged in LDS once per workgroup of NW waves (short rows)
     HOPXL(8, 2, 16, 4),
     HOPXL(8, 2, 8, 4),
