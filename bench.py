@@ -169,6 +169,7 @@ def main():
     kt = eng.kernel_ms()
     eng.kernel_timing(0)
 
+    kernel_by_rank = per_rank(kt.avg_ms, distributed, local)
     t = torch.tensor([elapsed, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -261,6 +262,7 @@ def main():
                 "traffic": traffic,
                 "kernel": kernel_name(sh) + ", per GPU",
                 "kernel_ms": round(kernel_ms, 5),
+                "kernel_ms_by_rank": kernel_by_rank,
                 "bytes_per_launch": per_gpu,
                 "traffic_source": traffic_src,
             },
@@ -405,10 +407,13 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             el = time.perf_counter() - t0
             kt = e.kernel_ms()
             e.kernel_timing(0)
+            by_rank[0] = per_rank(kt.avg_ms, distributed, local)
             t = torch.tensor([el, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
             if distributed:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t[0]), float(t[1])
+
+        by_rank = [None]
 
         total = sum(8 * (s.n_rows * s.n_cols + s.n_cols + (R if alg == "colwise" else s.y_len))
                     for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
@@ -421,6 +426,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 e.multiply()
             e.sync()
             el, kms = timed(e, args.config_steps)
+            tree_by_rank = by_rank[0]
             y = e.collect()
             yx = None
             if rank == 0:
@@ -440,6 +446,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
                          "gflops": round(2 * R * C * xsteps / xel / 1e9, 1),
                          "steps": xsteps, "kernel": xkernel, "kernel_ms": round(xkms, 5),
+                         "kernel_ms_by_rank": by_rank[0],
                          "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
                 if rank == 0:
                     rel = float(np.max(np.abs(yx - y) / np.abs(y)))
@@ -454,7 +461,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             "value": round(total * args.config_steps / el / 1e9, 1), "unit": "GB/s",
             "ms_per_step": round(el / args.config_steps * 1e3, 4), "steps": args.config_steps,
             "gflops": round(2 * R * C * args.config_steps / el / 1e9, 1),
-            "kernel": kernel_name(sh), "kernel_ms": round(kms, 5),
+            "kernel": kernel_name(sh), "kernel_ms": round(kms, 5), "kernel_ms_by_rank": tree_by_rank,
             "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
             "exact": exact,
         }
@@ -529,6 +536,20 @@ def parse_rccl_log(lines):
         if m and "Init COMPLETE" in line:
             nranks.append(int(m.group(1)))
     return {"links": {k: sorted(v) for k, v in links.items()}, "nranks": nranks, "samples": samples}
+
+
+def per_rank(ms, distributed, local):
+    """Every rank's mean GEMV time (ms), in rank order (None at N = 1): the max over ranks is the
+    step's kernel time, the spread shows whether one GPU lags the others."""
+    if not distributed:
+        return None
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([ms], dtype=torch.float64, device=f"cuda:{local}")
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [round(float(v[0]), 5) for v in out]
 
 
 def rccl_report(path, distributed, rank):
