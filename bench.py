@@ -19,10 +19,15 @@ reference cannot run), `end_to_end` (distribution from the root's host memory + 
 the root, the reference's timing semantics), and `configs`: BASELINE.json configs 3-5 at their
 own fixed sizes on the same N GPUs (strong scaling, device-resident, same engine, same step),
 so one scaling run covers every multi-GPU config (each also in bit-exact mode, `configs[].exact`);
-supplementary, never `value`. `exact`: the
-same workload with the engine in bit-exact mode (mvg_engine_set_exact: y identical to the
-reference's sequential sums), its step rate and kernel roofline fraction, and (rank 0, N = 1,
-row split) its y compared bit for bit with the oracle port's and the real reference's.
+supplementary, never `value`. Each config carries `reference_rows` (its y against the real
+reference's own y on four bands of its rows at P = N, tests/golden/config_slices.npz) and, at
+N = 1, a `cpu_baseline` of its own (the reference on a 64 MiB row slice, the -O2 port on the
+whole config up to 35 GB). `exact`: the same workload with the engine in bit-exact mode
+(mvg_engine_set_exact: y identical to the reference's sequential sums) — repeated multiplies on
+the engine's column-panel copy, and `row_major`, the kernels a fresh distribution runs — its step
+rate and kernel roofline fraction, and (rank 0, N = 1, row split) its y compared bit for bit with
+the oracle port's and the real reference's. At N > 1: `rccl` (the transport RCCL chose for every
+connection and the communicator sizes, from its NCCL_DEBUG=INFO log) and `kernel_ms_by_rank`.
 """
 from __future__ import annotations
 
