@@ -746,14 +746,15 @@ constexpr int seq_id(const T (&table)[N], const char* name) {
 constexpr int kSeqScalar = seq_id(kSeqVariants, "seq_scalar");
 constexpr int kSeqManyRows = seq_id(kSeqVariants, "seqx_r64_t16_b2_g8");
 constexpr int kHopRows = seq_id(kSeqVariants, "hop8_l8_w2_u16");
+constexpr int kHopLongRows = seq_id(kSeqVariants, "hop8_l8_w2_u24");
 constexpr int kHopWide = seq_id(kSeqVariants, "hop8_l16_w4_u8");
 constexpr int kHopWidest = seq_id(kSeqVariants, "hop8_l16_w8_u4");
 constexpr int kHopFewRows = seq_id(kSeqVariants, "hop8_l32_w8_u4");
 static_assert(kSeqScalar > 0 && kSeqVariants[kSeqScalar].needs == kAnyOperands, "8-B exact fallback");
-static_assert(kSeqManyRows > 0 && kHopRows > 0 && kHopWide > 0 && kHopWidest > 0 &&
+static_assert(kSeqManyRows > 0 && kHopRows > 0 && kHopLongRows > 0 && kHopWide > 0 && kHopWidest > 0 &&
                   kHopFewRows > 0,
               "exact dispatch names a missing variant");
-static_assert(kSeqVariants[kHopRows].needs == kAnyOperands &&
+static_assert(kSeqVariants[kHopRows].needs == kAnyOperands && kSeqVariants[kHopLongRows].needs == kAnyOperands &&
                   kSeqVariants[kHopWide].needs == kAnyOperands && kSeqVariants[kHopWidest].needs == kAnyOperands &&
                   kSeqVariants[kHopFewRows].needs == kAnyOperands,
               "the chain-hopping picks take any operands");
@@ -765,8 +766,9 @@ static_assert(kSeqVariants[kHopRows].needs == kAnyOperands &&
 // multiple of 16) with 2048 < K < 65536 — 64-row waves of 256-B row segments (the strips and
 // blocks of configs 3 and 4: 622 against 663 us, 2461 against 2490). Everything else takes the
 // chain-hopping forms, with 8-B loads (they equal the 16-B ones on aligned data and take any
-// lda): 8 lanes x 16 B per row from 6144 rows (or K <= 8192; round 3 dropped the 24-segment
-// form for K >= 65536, which gained 0.1-1.9 %), 16 lanes x 32 B for 2048 .. 6143 rows (x 64 B below 4096 rows with K >= 32768),
+// lda): 8 lanes x 16 B per row from 6144 rows (or K <= 8192; 24 segments in flight from
+// K = 65536: 131072^2 19.8 against 20.4 ms, 2.9 %, profiles/r03/sweep_exact_u16_u24_big.jsonl;
+// level at 65536^2), 16 lanes x 32 B for 2048 .. 6143 rows (x 64 B below 4096 rows with K >= 32768),
 // 32 lanes x 64 B for fewer rows with K > 4096, where the chain dominates (the reference's
 // R x 60000: 1200 rows in 203 us, 679 with the LDS forms), 16 x 32 B for short ones. On rows
 // that start mid-line they beat the tree form itself (16384 x 16386: 305 us against 315);
@@ -774,7 +776,7 @@ static_assert(kSeqVariants[kHopRows].needs == kAnyOperands &&
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
     if (lines && operands_ok(kVec16Lda23, lda, aligned) && M >= 32768 && K > 2048 && K < 65536)
         return kSeqManyRows;
-    if (M >= 6144) return kHopRows;
+    if (M >= 6144) return K >= 65536 ? kHopLongRows : kHopRows;
     if (M >= 2048) return K <= 8192 ? kHopRows : M < 4096 && K >= 32768 ? kHopWidest : kHopWide;
     return K <= 4096 ? kHopWide : kHopFewRows;
 }
