@@ -45,8 +45,15 @@ def test_reference_rows_check(cfg_name, alg, R, C, n):
     y[rows[0]] *= 1 + 1e-10
     with pytest.raises(AssertionError):
         bench.reference_rows_check(cfg_name, alg, R, C, n, y, None)
-    # no reference slice at this P: recorded, not checked
-    assert bench.reference_rows_check(cfg_name, alg, R, C, 3, y, None)["checked"] is False
+    # no reference slice at this P: recorded, not checked — except the row split, whose row sums
+    # do not depend on P (its P = 1 slice stands for every P)
+    r3 = bench.reference_rows_check(cfg_name, alg, R, C, 3, y, None) if alg != "rowwise" else None
+    if r3 is not None:
+        assert r3["checked"] is False
+    else:
+        y[rows[0]] = want[0]
+        r = bench.reference_rows_check(cfg_name, alg, R, C, 4, y, None)
+        assert r["P"] == 4 and r["max_rel"] == 0.0 and "at P1" in r["source"]
 
 
 def test_sample_splits_follow_the_reference_checks():
