@@ -240,6 +240,8 @@ def test_bench_two_ranks_one_device(tmp_path):
         ref = cfg[name]["reference_rows"]
         assert ref["P"] == 2 and ref["rows"] == 512 and ref["max_rel"] <= 1e-12, ref
         assert ref["exact_bit_identical"], ref  # grids of <= 2 columns: deterministic reference sums
+    # the weak-scaled main workload's first rows are config 2's: against the reference's rows too
+    assert d["reference_rows"]["max_rel"] <= 1e-12 and d["reference_rows"]["exact_bit_identical"], d["reference_rows"]
     # the transports RCCL reported for its connections (loopback sockets here: both ranks on GPU 0)
     assert d["rccl"]["logged"] and 2 in d["rccl"]["comm_sizes"] and d["rccl"]["transport_counts"], d["rccl"]
 
