@@ -4,7 +4,8 @@
  * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
  * cpu_baseline leg may load this (as the checker / the CPU baseline), never the product
  * path. It is pinned against golden y vectors produced by the real reference (compiled
- * from /root/reference/src with MPICH by oracle/build_ref.sh, see tests/golden/README.md).
+ * from /root/reference/src with MPICH by oracle/build_ref.sh; tests/golden/make_golden.py and
+ * tests/golden/make_config_slices.py run it).
  *
  * Every function cites the reference file:line it restates. Arithmetic is plain C with
  * -ffp-contract=off (no FMA), exactly the operation order of the reference:
