@@ -407,3 +407,21 @@ def test_exact_panel_dispatch_and_argument_checks():
     # nothing to do is not an error (no launch either)
     assert lib.mvg_gemv_exact_panels(None, 0, 256, None, None, 0, 1000, 0, None) == 0
     assert lib.mvg_panel_relayout(None, 0, 0, 0, None, 0, 256, None) == 0
+
+
+def test_gendata_writes_the_reference_inputs(tmp_path):
+    # python -m matvec_mpi_multiplier_amd.gendata: ./data/matrix_R_C.txt + vector_C.txt in the
+    # reference's "%.4f" format (the generator its repository lacks), values = the synthetic spec
+    from matvec_mpi_multiplier_amd import gendata
+    from oracle import oracle
+
+    d = str(tmp_path / "data")
+    gendata.main(["6", "10", "3", "10", "--dir", d])
+    assert sorted(os.listdir(d)) == ["matrix_3_10.txt", "matrix_6_10.txt", "out", "vector_10.txt"]
+    np.testing.assert_array_equal(mm.load_matr(6, 10, d), oracle.synth(6, 10, 42))
+    np.testing.assert_array_equal(mm.load_matr(3, 10, d), oracle.synth(3, 10, 42))
+    np.testing.assert_array_equal(mm.load_vec(10, d), oracle.synth(1, 10, 4242)[0])
+    assert open(os.path.join(d, "matrix_3_10.txt")).read().split()[0] == "%.4f" % oracle.synth(1, 1, 42)[0, 0]
+    assert gendata.TEST_SH_SIZES == (600, 1800, 3000, 4200, 5400, 6600, 7800, 9000, 10200)
+    with pytest.raises(SystemExit):
+        gendata.main(["6"])

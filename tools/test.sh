@@ -3,7 +3,8 @@
 #   tools/test.sh <rowwise|colwise|blockwise> [P ...]
 # Runs `mpiexec -n P bin/multiplier_<alg> n n` for the reference's nine square sizes, from the
 # current directory (which must hold ./data/matrix_n_n.txt, ./data/vector_n.txt and
-# ./data/out/, as for the reference; MVG_SYNTH=1 generates the inputs instead). Rows go to
+# ./data/out/, as for the reference — `python -m matvec_mpi_multiplier_amd.gendata --test-sh` writes
+# them; MVG_SYNTH=1 generates the inputs in memory instead). Rows go to
 # ./data/out/<alg>.csv in the reference's format. P defaults to 1 2 4 8 (one MI355X per rank;
 # the reference's 1 2 6 12 24 counted CPU processes). Set MPIEXEC to use another launcher.
 set -e
