@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--config-cpu-sample-bytes", type=float, default=3.5e10,
                     help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
     ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--no-multi", action="store_true", help="skip the multi-vector GEMV section")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the bit-exact section (the same workload with mvg_engine_set_exact)")
     return ap.parse_args()
@@ -203,6 +204,11 @@ def main():
     if not args.no_exact:
         exact, y_exact = exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, total_bytes, y)
 
+    # ---- several x per pass over A, rank 0 at N = 1
+    multi = None
+    if rank == 0 and n == 1 and not args.no_multi:
+        multi = multi_vector_section(local)
+
     # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
     e2e = None
     if not args.no_e2e and args.e2e_iters > 0:
@@ -277,6 +283,7 @@ def main():
             "reference_rows": ref_rows,
             "rccl": rccl,
             "exact": exact,
+            "multi_vector": multi,
             "end_to_end": e2e,
             "configs": configs,
         }
@@ -358,6 +365,61 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
         assert np.array_equal(y, y_rm), "the panel and row-major exact kernels differ"
         out["max_rel_vs_tree"] = rel
     return out, y
+
+
+def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
+    """mvg_gemv_multi (several x per pass over A; beyond the reference) on a
+    config-2-sized A: for nv = 2, 4, 8 the kernel's mean time (HIP events, `launches` back to
+    back), the rate at which it reads A and its algorithmic bytes (A once, every x and y), and
+    the speed-up over nv separate mvg_gemv calls timed the same way. Each vector's y is checked
+    against the single-vector kernel's (<= 1e-12)."""
+    import torch
+
+    from matvec_mpi_multiplier_amd import multiplier as mm
+    from matvec_mpi_multiplier_amd._lib import check, lib
+
+    s = torch.cuda.current_stream(local).cuda_stream
+    nvmax = 8
+    dA, dX, dY, dy = mm.DeviceBuffer(M * K), mm.DeviceBuffer(K * nvmax), mm.DeviceBuffer(M * nvmax), mm.DeviceBuffer(M)
+    try:
+        check(lib.mvg_synth_fill_device(dA.ptr, K, M, K, 0, 0, K, 42, s), "fill A")
+        for v in range(nvmax):  # vector v: seed 4242 + v
+            check(lib.mvg_synth_fill_device(dX.ptr + 8 * K * v, K, 1, K, 0, 0, K, 4242 + v, s), "fill x")
+
+        def t(fn):
+            fn()
+            torch.cuda.synchronize(local)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(launches):
+                fn()
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1) / launches
+
+        single = t(lambda: lib.mvg_gemv(dA.ptr, K, dX.ptr, dy.ptr, M, K, s))
+        out = {"shape": [M, K], "single_ms": round(single, 5), "nv": {}}
+        worst = 0.0
+        for nv in (2, 4, 8):
+            ms = t(lambda: lib.mvg_gemv_multi(dA.ptr, K, dX.ptr, K, dY.ptr, M, M, K, nv, s))
+            Y = dY.download(M * nv).reshape(nv, M)
+            for v in range(nv):
+                check(lib.mvg_gemv(dA.ptr, K, dX.ptr + 8 * K * v, dy.ptr, M, K, s), "gemv")
+                check(lib.mvg_stream_sync(s), "sync")
+                y1 = dy.download()
+                worst = max(worst, float(np.max(np.abs(Y[v] - y1) / np.abs(y1))))
+            out["nv"][str(nv)] = {
+                "kernel_ms": round(ms, 5),
+                "A_GBps": round(8 * M * K / (ms * 1e-3) / 1e9, 1),
+                "algorithmic_GBps": round(8 * (M * K + nv * (K + M)) / (ms * 1e-3) / 1e9, 1),
+                "speedup_vs_separate": round(nv * single / ms, 3),
+            }
+        assert worst <= 1e-12, f"multi-vector y differs from the single-vector y by {worst}"
+        out["max_rel_vs_single"] = worst
+        return out
+    finally:
+        for b in (dA, dX, dY, dy):
+            b.free()
 
 
 def exact_kernel_name(eng) -> str:
