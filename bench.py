@@ -80,6 +80,7 @@ def parse():
                     help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
     ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-vector GEMV section")
+    ap.add_argument("--no-loader", action="store_true", help="skip the text-loader section")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the bit-exact section (the same workload with mvg_engine_set_exact)")
     return ap.parse_args()
@@ -209,6 +210,11 @@ def main():
     if rank == 0 and n == 1 and not args.no_multi:
         multi = multi_vector_section(local)
 
+    # ---- the text loader on config 2's input file, rank 0 at N = 1
+    loader = None
+    if rank == 0 and n == 1 and not args.no_loader:
+        loader = loader_section(R, C)
+
     # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
     e2e = None
     if not args.no_e2e and args.e2e_iters > 0:
@@ -284,6 +290,7 @@ def main():
             "rccl": rccl,
             "exact": exact,
             "multi_vector": multi,
+            "loader": loader,
             "end_to_end": e2e,
             "configs": configs,
         }
@@ -420,6 +427,41 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
     finally:
         for b in (dA, dX, dY, dy):
             b.free()
+
+
+def loader_section(R, C):
+    """The reference's input file for this workload (./data/matrix_R_C.txt, "%.4f" tokens,
+    matr_utils.c:42-62), written to a scratch directory and read back by mvg_load_matr (mmap +
+    threads, bit-identical to fscanf "%lf"): its parse rate on this host, and the matrix it gives
+    against the synthetic generator's, bit for bit. The file is removed afterwards."""
+    import shutil
+    import tempfile
+
+    from matvec_mpi_multiplier_amd import multiplier as mm
+
+    work = tempfile.mkdtemp(prefix="mvg_loader_")
+    try:
+        path = os.path.join(work, mm.build_matrix_filename(R, C))
+        t0 = time.perf_counter()
+        mm.write_matr_synth(path, R, C, 42)
+        wrote = time.perf_counter() - t0
+        nbytes = os.path.getsize(path)
+        best = None
+        for _ in range(2):  # the first pass also pages the file in
+            t0 = time.perf_counter()
+            A = mm.load_matr(R, C, work)
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        same = bool(np.array_equal(A, mm.synth_host(R, C, 42)))
+        assert same, "the loader's matrix differs from the synthetic values its file holds"
+        del A
+        return {"file": os.path.basename(path), "text_bytes": nbytes, "parse_s": round(best, 4),
+                "GBps_text": round(nbytes / best / 1e9, 2), "write_s": round(wrote, 3),
+                "threads": os.cpu_count(), "bit_identical_to_values": same,
+                "note": "mmap + threads, Clinger's fast path, strtod otherwise (fscanf's values); "
+                        "the reference's fscanf reads the same file token by token"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
 
 
 def exact_kernel_name(eng) -> str:

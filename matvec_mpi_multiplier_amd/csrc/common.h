@@ -55,14 +55,16 @@ __host__ __device__ inline double synth_value(uint64_t s0, uint64_t idx) {
     return (double)mulhi_10000(z) / 10000.0;
 }
 
-// Static split of [0, n) over the host's threads (capped by MVG_THREADS / 64).
-// `serial` forces one thread (small jobs).
+// Host threads the library's CPU work (loader, host generator, first touch) uses: $MVG_THREADS
+// if set, else the CPUs this process may actually run on — its affinity mask, capped by its
+// cgroup's CPU quota (a job given 16 CPUs of a 256-CPU host sees 256 in hardware_concurrency) —
+// at most 64 (host.cpp).
+int host_thread_count();
+
+// Static split of [0, n) over host_thread_count() threads. `serial` forces one thread.
 template <class F>
 void parallel_for(int64_t n, F&& body, bool serial = false) {
-    int nt = (int)std::thread::hardware_concurrency();
-    if (const char* e = getenv("MVG_THREADS")) nt = atoi(e);
-    if (nt < 1) nt = 1;
-    if (nt > 64) nt = 64;
+    int nt = host_thread_count();
     if (nt > n) nt = (int)(n > 0 ? n : 1);
     if (serial || nt == 1) {
         body((int64_t)0, n);

@@ -30,6 +30,31 @@ int hip_fail(hipError_t e, const char* what) {
     return MVG_E_HIP;
 }
 
+// ------------------------------------------------------------------ host threads
+int host_thread_count() {
+    if (const char* e = getenv("MVG_THREADS")) {
+        const int v = atoi(e);
+        return v < 1 ? 1 : v > 64 ? 64 : v;
+    }
+    static const int n = [] {
+        int nt = (int)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) nt = CPU_COUNT(&set);
+        // cgroup v2 quota: "<max> <period>" in cpu.max ("max" = unlimited)
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            long long period = 0;
+            if (fscanf(f, "%31s %lld", q, &period) == 2 && period > 0 && strcmp(q, "max") != 0) {
+                const long long cpus = (atoll(q) + period - 1) / period;
+                if (cpus >= 1 && cpus < nt) nt = (int)cpus;
+            }
+            fclose(f);
+        }
+        return nt < 1 ? 1 : nt > 64 ? 64 : nt;
+    }();
+    return n;
+}
+
 }  // namespace mvg
 
 using namespace mvg;

@@ -236,10 +236,7 @@ int parse_file(const std::string& path, int64_t n, double* out) {
     close(fd);
     if (base == MAP_FAILED) return fail(MVG_E_IO, "mmap failed for '" + path + "'");
 
-    int nt = (int)std::thread::hardware_concurrency();
-    if (const char* e = getenv("MVG_THREADS")) nt = atoi(e);
-    if (nt < 1) nt = 1;
-    if (nt > 64) nt = 64;
+    int nt = host_thread_count();
     if (len < (1u << 20)) nt = 1;
     // nr = nt * kStreams ranges, range r = [cut[r], cut[r+1]), thread t taking ranges
     // [t*kStreams, +kStreams); cuts moved forward to the next whitespace so that no token
