@@ -429,6 +429,21 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
             b.free()
 
 
+def host_threads():
+    """The library's host thread count (csrc/host.cpp host_thread_count): $MVG_THREADS, else the
+    process's CPUs capped by its cgroup quota, at most 64."""
+    if os.environ.get("MVG_THREADS"):
+        return max(1, min(64, int(os.environ["MVG_THREADS"])))
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(period) > 0:
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(64, n))
+
+
 def loader_section(R, C):
     """The reference's input file for this workload (./data/matrix_R_C.txt, "%.4f" tokens,
     matr_utils.c:42-62), written to a scratch directory and read back by mvg_load_matr (mmap +
@@ -457,7 +472,7 @@ def loader_section(R, C):
         del A
         return {"file": os.path.basename(path), "text_bytes": nbytes, "parse_s": round(best, 4),
                 "GBps_text": round(nbytes / best / 1e9, 2), "write_s": round(wrote, 3),
-                "threads": os.cpu_count(), "bit_identical_to_values": same,
+                "threads": host_threads(), "bit_identical_to_values": same,
                 "note": "mmap + threads, Clinger's fast path, strtod otherwise (fscanf's values); "
                         "the reference's fscanf reads the same file token by token"}
     finally:
