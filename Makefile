@@ -14,7 +14,7 @@ LDLIBS   := -L$(ROCM)/lib -lamdhip64 -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
 
 HIP_SRCS := $(CSRC)/gemv.hip $(CSRC)/gemv_exact.hip
 CXX_SRCS := $(CSRC)/host.cpp $(CSRC)/engine.cpp $(CSRC)/textio.cpp
-HDRS     := $(CSRC)/common.h include/matvec_gpu.h
+HDRS     := $(CSRC)/common.h $(CSRC)/lds_dma.h include/matvec_gpu.h
 OBJS     := $(BUILD)/gemv.o $(BUILD)/gemv_exact.o $(BUILD)/host.o $(BUILD)/engine.o $(BUILD)/textio.o
 APPS     := bin/multiplier_rowwise bin/multiplier_colwise bin/multiplier_blockwise
 

@@ -170,6 +170,9 @@ int mvg_gemv_multi(const double* d_A, int64_t lda, const double* d_X, int64_t ld
 int mvg_gemv_multi_variant(const double* d_A, int64_t lda, const double* d_X, int64_t ldx, double* d_Y,
                            int64_t ldy, int64_t m, int64_t k, int nv, int variant, void* stream);
 int mvg_gemv_multi_variant_count(void);
+/* the variant mvg_gemv_multi picks for each group of up to 8 of nv >= 2 vectors (16-B aligned A
+ * and X, even lda and ldx); 0 for nv < 2 (the single-vector dispatch) */
+int mvg_gemv_multi_auto_variant(int64_t lda, int64_t ldx, int64_t m, int64_t k, int nv);
 const char* mvg_gemv_multi_variant_name(int variant);
 
 /* Bit-exact form of mvg_gemv: every row is the reference's own chain

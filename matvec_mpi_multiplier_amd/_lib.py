@@ -108,6 +108,7 @@ SIGNATURES = {
     "mvg_gemv_multi": (C.c_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, C.c_int, _p]),
     "mvg_gemv_multi_variant": (C.c_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, C.c_int, C.c_int, _p]),
     "mvg_gemv_multi_variant_count": (C.c_int, []),
+    "mvg_gemv_multi_auto_variant": (C.c_int, [_i64, _i64, _i64, _i64, C.c_int]),
     "mvg_gemv_multi_variant_name": (C.c_char_p, [C.c_int]),
     "mvg_gemv_exact": (C.c_int, [_p, _i64, _p, _p, _i64, _i64, _p]),
     "mvg_multiply_std_rowwise": (C.c_int, [_p, _p, _i64, _i64, _p, C.c_int]),

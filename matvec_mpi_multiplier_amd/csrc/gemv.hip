@@ -19,6 +19,7 @@
 // global_load_dwordx4, which gfx950 serves unaligned. Only a base off an 8-B boundary falls back
 // to the scalar variants (8 B per lane, still coalesced).
 #include "common.h"
+#include "lds_dma.h"
 
 #include <map>
 #include <mutex>
@@ -1243,6 +1244,188 @@ __global__ __launch_bounds__(kBlock) void gemv_mxres(const double* __restrict__ 
         }
 }
 
+// A through LDS by DMA (mid and long rows, nv >= 2). The register forms above keep A's loads in
+// flight in VGPRs next to RPG x NV accumulators, which at nv = 8 leaves room for too little A
+// (r01: 5.6 TB/s of A at 16384^2 against 7.0 for one vector). Here A never passes through
+// VGPRs on its way in: workgroup b owns rows [16*RQ*b, +16*RQ) and its NW waves split the column
+// tiles (wave w takes tiles w, w + NW, ...: the workgroup sweeps its rows' columns in order, a
+// sliding window over A as in gemv_rowblock). A tile is 16*RQ rows x 2T columns, loaded with
+// `global_load_lds_dwordx4` (nt) into a per-wave ring of NB buffers together with the tile's x
+// segment for all NV vectors (linear, [v][chunk]); NB-1 tiles in flight behind the one summed.
+//   swizzle: LDS slot s of row r holds the row's 16-B chunk s ^ (r & 15), so the compute reads
+//            below are conflict-free over every ds_read_b128 lane group;
+//   compute: lane (i = l & 15, g = l >> 4) takes chunk 4s + g of rows i + 16q (q < RQ) at step s
+//            (one ds_read_b128 per row) and the same chunk of each vector's x (a 4-address
+//            broadcast), and adds its 2*RQ*NV FMAs into acc[q][v];
+//   reduce : over g (xor 16, 32), then over the waves in wave order through LDS — fixed order,
+//            deterministic. The column tail (K % 2T) is summed from global memory.
+// Needs 16-B aligned A and X with even lda and ldx, 16*RQ rows of lda and NV rows of ldx within
+// 32-bit byte offsets (host-checked: dma_ok).
+template <int RQ, int T, int NB, int NW, int NV, int ROT>
+__global__ __launch_bounds__(NW * 64) void gemv_mdma(const double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ X, int64_t ldx,
+                                                     double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                     int64_t K, int nv) {
+    static_assert(T == 16 || T == 32 || T == 64, "tile width: 16, 32 or 64 chunks of 16 B");
+    constexpr int RB = 16 * RQ;                   // rows per workgroup
+    constexpr int kRows = 64 / T;                 // rows one DMA instruction fills (1 KiB)
+    constexpr int kInst = RB / kRows;             // A instructions per tile
+    constexpr int kXInst = (NV * T + 63) / 64;    // x instructions per tile
+    constexpr int kPer = kInst + kXInst;
+    static_assert(kPer * (NB - 1) <= 63, "loads in flight must fit the vmcnt counter");
+    constexpr int kCols = 2 * T;
+    constexpr int kRowBytes = 16 * T;
+    constexpr int kTileBytes = RB * kRowBytes;
+    constexpr int kBufBytes = kTileBytes + kXInst * 1024;
+    static_assert(NB * kBufBytes >= RQ * NV * 16 * (int)sizeof(double), "partials fit the ring");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NW][NB * kBufBytes];
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * RB;
+    const int64_t ntiles = K / kCols;
+    unsigned char* const ring = lds[w];
+
+    // DMA side: A instruction j, lane -> tile row j*kRows + lane/T (rows past M re-read the
+    // last row), LDS slot lane%T; x instruction j, lane -> flat [v][chunk] index 64j + lane
+    // (vectors past nv re-read vector 0, indices past NV*T land in the padding).
+    uint32_t aoff[kInst], xoff[kXInst];
+#pragma unroll
+    for (int j = 0; j < kInst; ++j) {
+        const int row = j * kRows + lane / T;
+        const int64_t rr = r0 + row < M ? row : M - 1 - r0;
+        aoff[j] = (uint32_t)((rr * lda + 2 * ((lane % T) ^ (row & 15))) * (int64_t)sizeof(double));
+    }
+#pragma unroll
+    for (int j = 0; j < kXInst; ++j) {
+        int q = 64 * j + lane;
+        q = q < NV * T ? q : NV * T - 1;
+        const int v = q / T;
+        xoff[j] = (uint32_t)(((v < nv ? v : 0) * ldx + 2 * (q % T)) * (int64_t)sizeof(double));
+    }
+    const unsigned char* const a0 = reinterpret_cast<const unsigned char*>(A + r0 * lda);
+    const unsigned char* const x0 = reinterpret_cast<const unsigned char*>(X);
+    // ROT > 0: workgroup b starts at tile b*ROT (mod ntiles) and wraps around, so workgroups in
+    // flight read different columns (rows a power-of-two stride apart otherwise hit the same
+    // HBM channels at the same time)
+    const int64_t rot = ROT > 0 && ntiles > 0 ? ((int64_t)blockIdx.x * ROT) % ntiles : 0;
+    auto issue = [&](int64_t t, int b) {
+        t += rot;
+        if (t >= ntiles) t -= ntiles;
+        const int64_t colb = t * kCols * (int64_t)sizeof(double);
+        unsigned char* buf = ring + b * kBufBytes;
+#pragma unroll
+        for (int j = 0; j < kInst; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(a0 + colb + aoff[j]), (lds_void_t)(buf + j * 1024),
+                                             16, 0, 2 /* nt */);
+#pragma unroll
+        for (int j = 0; j < kXInst; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(x0 + colb + xoff[j]),
+                                             (lds_void_t)(buf + kTileBytes + j * 1024), 16, 0, 0);
+    };
+
+    const int i = lane & 15;
+    const int g = lane >> 4;
+    double acc[RQ][NV];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[q][v] = 0.0;
+    auto consume = [&](int b) {
+        const unsigned char* buf = ring + b * kBufBytes;
+#pragma unroll
+        for (int s = 0; s < T / 4; ++s) {
+            const int c = 4 * s + g;
+            dbl2 a[RQ], xx[NV];
+#pragma unroll
+            for (int q = 0; q < RQ; ++q)
+                a[q] = *reinterpret_cast<const dbl2*>(buf + (i + 16 * q) * kRowBytes + 16 * (c ^ i));
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                xx[v] = *reinterpret_cast<const dbl2*>(buf + kTileBytes + 16 * (v * T + c));
+#pragma unroll
+            for (int q = 0; q < RQ; ++q)
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    acc[q][v] = __builtin_fma(a[q].x, xx[v].x, acc[q][v]);
+                    acc[q][v] = __builtin_fma(a[q].y, xx[v].y, acc[q][v]);
+                }
+        }
+    };
+
+    const int64_t nt = ntiles > w ? (ntiles - w + NW - 1) / NW : 0;  // this wave's tiles
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p)
+        if (p < nt) issue(w + (int64_t)NW * p, p);
+    for (int64_t u = 0; u < nt; ++u) {
+        const int64_t un = u + NB - 1;
+        if (un < nt) {
+            // buffer un % NB was summed in iteration u-1; its ds_reads have returned (their
+            // values fed the FMAs), the wait only keeps the order explicit
+            wait_lgkmcnt0();
+            issue(w + (int64_t)NW * un, (int)(un % NB));
+            wait_vmcnt<kPer*(NB - 1)>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        consume((int)(u % NB));
+    }
+
+    // column tail: column c of rows i + 16q, columns spread over the waves and the four g lanes
+    for (int64_t c = ntiles * kCols + 4 * w + g; c < K; c += 4 * NW) {
+#pragma unroll
+        for (int q = 0; q < RQ; ++q) {
+            const int64_t rr = r0 + i + 16 * q < M ? r0 + i + 16 * q : M - 1;
+            const double a = A[rr * lda + c];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) acc[q][v] = __builtin_fma(a, X[(v < nv ? v : 0) * ldx + c], acc[q][v]);
+        }
+    }
+
+#pragma unroll
+    for (int q = 0; q < RQ; ++q)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            acc[q][v] += __shfl_xor(acc[q][v], 16, 64);
+            acc[q][v] += __shfl_xor(acc[q][v], 32, 64);
+        }
+    if constexpr (NW == 1) {
+#pragma unroll
+        for (int q = 0; q < RQ; ++q)
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (g == 0 && r0 + i + 16 * q < M && v < nv) Y[v * ldy + r0 + i + 16 * q] = acc[q][v];
+    } else {
+        // partials [q][v][i] in the wave's own ring (all its DMA retired and its reads consumed)
+        wait_vmcnt<0>();
+        wait_lgkmcnt0();
+        double* part = reinterpret_cast<double*>(ring);
+        if (g == 0) {
+#pragma unroll
+            for (int q = 0; q < RQ; ++q)
+#pragma unroll
+                for (int v = 0; v < NV; ++v) part[(q * NV + v) * 16 + i] = acc[q][v];
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < RQ * NV * 16; t += NW * 64) {
+            const int ii = t % 16, v = (t / 16) % NV, q = t / (16 * NV);
+            const int64_t row = r0 + ii + 16 * q;
+            if (row < M && v < nv) {
+                double s = 0.0;
+#pragma unroll
+                for (int ww = 0; ww < NW; ++ww) s += reinterpret_cast<const double*>(lds[ww])[t];
+                Y[v * ldy + row] = s;
+            }
+        }
+    }
+}
+
+// host side of gemv_mdma's address limits: 16*RQ rows of A and NV rows of X in 32-bit offsets
+inline bool dma_ok(int rows_per_block, int64_t lda, int64_t ldx) {
+    return (int64_t)rows_per_block * lda * (int64_t)sizeof(double) < (1ll << 31) &&
+           8 * ldx * (int64_t)sizeof(double) < (1ll << 31);
+}
+
 typedef void (*gemv_multi_fn)(const double*, int64_t, const double*, int64_t, double*, int64_t, int64_t,
                               int64_t, int);
 
@@ -1251,6 +1434,7 @@ struct MultiVariant {
     gemv_multi_fn fn[3];  // NV = 2, 4, 8
     int rows_per_block;
     int block;
+    bool dma = false;     // gemv_mdma: 32-bit DMA offsets (dma_ok)
 };
 
 #define MVEC(LPR, RPG, UNR)                                                                              \
@@ -1270,6 +1454,16 @@ struct MultiVariant {
     {"mxres_l" #LPR "_r" #RPG "_u" #UNR,                                                                 \
      {gemv_mxres<LPR, RPG, 2, UNR>, gemv_mxres<LPR, RPG, 4, UNR>, gemv_mxres<LPR, RPG, 8, UNR>},         \
      (kBlock / 64) * (64 / LPR) * RPG, kBlock}
+
+#define MDMA(RQ, T, NB, NW)                                                                              \
+    {"mdma_r" #RQ "_t" #T "_b" #NB "_w" #NW,                                                             \
+     {gemv_mdma<RQ, T, NB, NW, 2, 0>, gemv_mdma<RQ, T, NB, NW, 4, 0>, gemv_mdma<RQ, T, NB, NW, 8, 0>},   \
+     16 * RQ, NW * 64, true}
+#define MDMAS(RQ, T, NB, NW, ROT)                                                                        \
+    {"mdma_r" #RQ "_t" #T "_b" #NB "_w" #NW "_s" #ROT,                                                   \
+     {gemv_mdma<RQ, T, NB, NW, 2, ROT>, gemv_mdma<RQ, T, NB, NW, 4, ROT>,                                \
+      gemv_mdma<RQ, T, NB, NW, 8, ROT>},                                                                 \
+     16 * RQ, NW * 64, true}
 
 static constexpr MultiVariant kMultiVariants[] = {
     {"auto", {nullptr, nullptr, nullptr}, 0, 0},  // 0
@@ -1308,13 +1502,28 @@ static constexpr MultiVariant kMultiVariants[] = {
     MXR(64, 2, 2),                                // 33
     MXR(32, 2, 2),                                // 34
     MXR(16, 8, 1),                                // 35
+    MDMA(2, 16, 3, 2),                            // 36 A through LDS by DMA
+    MDMA(2, 16, 4, 2),                            // 37
+    MDMA(2, 16, 2, 4),                            // 38
+    MDMA(1, 16, 2, 4),                            // 39
+    MDMA(4, 16, 2, 1),                            // 40
+    MDMA(2, 32, 2, 2),                            // 41
+    MDMA(1, 16, 3, 8),                            // 42
+    MDMAS(2, 16, 2, 4, 1),                        // 43 rotated starts
+    MDMAS(2, 16, 2, 4, 5),                        // 44
+    MDMAS(2, 16, 2, 4, 17),                       // 45
+    MDMAS(1, 16, 2, 4, 5),                        // 46
+    MDMAS(2, 16, 4, 2, 5),                        // 47
+    MDMAS(1, 16, 3, 2, 5),                        // 48
+    MDMAS(4, 16, 2, 1, 5),                        // 49
 };
 constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVariants[0]));
 
 // From the MI355X sweeps (tools/multi_bench.py -> profiles/r01/multi_sweep.jsonl, then
 // multi_sweep2_lds.jsonl with the LDS form and multi_sweep5_xres.jsonl with the x-resident form;
 // 8 shapes, K = 512 ... 65536): per (nv group, K class) the variant with the best geometric mean
-// of (rate / best rate on the shape): 0.93-1.0 per class, worst single shape 0.90.
+// of (rate / best rate on the shape): 0.93-1.0 per class, worst single shape 0.90. (K < 6144;
+// longer rows take the DMA forms, below.)
 constexpr int kMx16r4u2 = variant_id(kMultiVariants, "mxres_l16_r4_u2");
 constexpr int kMx16r4u1 = variant_id(kMultiVariants, "mxres_l16_r4_u1");
 constexpr int kMx32r2u2 = variant_id(kMultiVariants, "mxres_l32_r2_u2");
@@ -1327,8 +1536,25 @@ static_assert(kMx16r4u2 > 0 && kMx16r4u1 > 0 && kMx32r2u2 > 0 && kMv32r2u1 > 0 &
                   kMrow4r4u1 > 0 && kMlds2u2 > 0 && kMlds8u2 > 0,
               "multi-vector dispatch names a variant missing from kMultiVariants");
 
-int pick_multi_variant(int64_t m, int64_t k, int nvp) {
-    (void)m;
+// A through LDS by DMA (gemv_mdma), workgroups starting 5 tiles apart: 32 rows x 4 waves per
+// workgroup from 8192 rows — vector groups of 8 from K = 1024, of 3-4 from K = 1280, pairs from
+// K = 6144 — and 16 rows x 4 waves for 4096-8191 rows of K >= 8192. From the MI355X sweeps
+// (tools/multi_bench.py -> profiles/r03/multi_sweep_dma*.jsonl, 20 shapes): nv = 8 reads A at
+// 6.3-7.0 TB/s where the register forms above reached 4.5-6.2 (rows a power-of-two stride apart
+// need the staggered starts: 16-20 % without them), nv = 4 within 3 % of the best form or
+// better, pairs level or better on the long rows; below those sizes the forms above stay.
+constexpr int kMd2w4s5 = variant_id(kMultiVariants, "mdma_r2_t16_b2_w4_s5");
+constexpr int kMd1w4s5 = variant_id(kMultiVariants, "mdma_r1_t16_b2_w4_s5");
+static_assert(kMd2w4s5 > 0 && kMd1w4s5 > 0, "multi-vector dispatch names a missing DMA variant");
+
+int pick_multi_dma(int64_t m, int64_t k, int nvp) {
+    if (m >= 8192) return (nvp >= 8 ? k >= 1024 : nvp >= 4 ? k >= 1280 : k >= 6144) ? kMd2w4s5 : 0;
+    return m >= 4096 && k >= 8192 ? kMd1w4s5 : 0;
+}
+
+int pick_multi_variant(int64_t m, int64_t k, int nvp, int64_t lda, int64_t ldx) {
+    const int d = pick_multi_dma(m, k, nvp);
+    if (d > 0 && dma_ok(kMultiVariants[d].rows_per_block, lda, ldx)) return d;
     if (k <= 768) return nvp <= 4 ? kMx16r4u2 : kMx16r4u1;
     if (nvp <= 2) return k <= 1024 ? kMv32r2u1 : kMrow4r4u1;
     if (nvp <= 4) return k <= 1024 ? kMx32r2u2 : k < 6144 ? kMlds2u2 : kMlds8u2;
@@ -1426,6 +1652,12 @@ int mvg_gemv(const double* A, int64_t lda, const double* x, double* y, int64_t m
 
 int mvg_gemv_multi_variant_count(void) { return kNumMultiVariants; }
 
+int mvg_gemv_multi_auto_variant(int64_t lda, int64_t ldx, int64_t m, int64_t k, int nv) {
+    if (nv < 2) return 0;
+    const int g = nv < 8 ? nv : 8;
+    return pick_multi_variant(m, k, g <= 2 ? 2 : g <= 4 ? 4 : 8, lda, ldx);
+}
+
 const char* mvg_gemv_multi_variant_name(int v) {
     if (v < 0 || v >= kNumMultiVariants) return "invalid";
     return kMultiVariants[v].name;
@@ -1459,8 +1691,10 @@ int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_
             continue;
         }
         const int slot = g <= 2 ? 0 : g <= 4 ? 1 : 2;
-        const int v = variant ? variant : pick_multi_variant(m, k, 2 << slot);
+        const int v = variant ? variant : pick_multi_variant(m, k, 2 << slot, lda, ldx);
         const MultiVariant& mv = kMultiVariants[v];
+        if (mv.dma && !dma_ok(mv.rows_per_block, lda, ldx))
+            return fail(MVG_E_INVALID, "mvg_gemv_multi: lda or ldx too large for the DMA variant");
         // launches of < 2^32 threads each (the grid-size cap), row ranges in order
         const int64_t max_rows = ((1ll << 31) / mv.block) * mv.rows_per_block;
         for (int64_t r0 = 0; r0 < m; r0 += max_rows) {

@@ -34,6 +34,7 @@
 // arrives by plain coalesced loads into VGPRs, and the running sum hops from lane to lane by
 // DPP, still in column order.
 #include "common.h"
+#include "lds_dma.h"
 
 // hipcc contracts a*b + c into an FMA by default (-ffp-contract=fast); the reference rounds the
 // product first. Off for this whole file (the Makefile also passes -ffp-contract=off for it).
@@ -42,25 +43,6 @@
 namespace mvg {
 
 typedef double dbl2x __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) void* lds_void_t;
-typedef __attribute__((address_space(1))) void* gbl_void_t;
-
-// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8]; the
-// others left at "no wait"), fenced against compiler reordering of memory operations: the
-// LDS-DMA writes of the tile about to be read are complete once at most N vector-memory
-// operations of this wave are outstanding.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx950");
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-__device__ __forceinline__ void wait_lgkmcnt0() {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
 
 // The reference's step: a rounded product, then a rounded add (never fused: plain operators
 // under the pragma above; HIP's __dmul_rn/__dadd_rn are defined where contraction is on, and

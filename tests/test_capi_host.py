@@ -425,3 +425,19 @@ def test_gendata_writes_the_reference_inputs(tmp_path):
     assert gendata.TEST_SH_SIZES == (600, 1800, 3000, 4200, 5400, 6600, 7800, 9000, 10200)
     with pytest.raises(SystemExit):
         gendata.main(["6"])
+
+
+def test_multi_vector_dispatch_takes_dma_forms_on_long_rows():
+    # gemv.hip pick_multi_dma: A through LDS by DMA (staggered starts) for vector groups on
+    # long rows; the register forms elsewhere; never the DMA forms when 32 rows of lda exceed
+    # the kernel's 32-bit offsets
+    lib = _lib.lib
+    name = lambda m, k, nv, lda=None: lib.mvg_gemv_multi_variant_name(
+        lib.mvg_gemv_multi_auto_variant(lda or k, k, m, k, nv)).decode()
+    assert name(16384, 16384, 8) == name(16384, 16384, 2) == name(2097152, 1024, 8) == "mdma_r2_t16_b2_w4_s5"
+    assert name(4096, 65536, 4) == "mdma_r1_t16_b2_w4_s5"
+    assert not name(4200, 4200, 8).startswith("mdma")
+    assert not name(16384, 4096, 2).startswith("mdma")       # pairs: from K = 6144
+    assert not name(4194304, 512, 8).startswith("mdma")      # short rows: x resident in LDS
+    assert not name(16384, 16384, 8, lda=1 << 24).startswith("mdma")
+    assert lib.mvg_gemv_multi_auto_variant(16384, 16384, 16384, 16384, 1) == 0

@@ -317,7 +317,10 @@ def test_engine_multiply_before_inputs_is_state_error(comm1):
 
 
 @pytest.mark.parametrize("m,k,nv", [(257, 1000, 1), (64, 16384, 2), (130, 4096, 3), (33, 20000, 5), (9, 512, 8),
-                                    (100, 3000, 11), (50, 1001, 4)])
+                                    (100, 3000, 11), (50, 1001, 4),
+                                    # the automatic DMA forms, with row and tile tails
+                                    (8195, 1030, 8), (8200, 1290, 3), (8197, 6150, 2), (4099, 8194, 6),
+                                    (8192, 1024, 16)])
 def test_multi_vector_gemv(m, k, nv):
     A = oracle.synth(m, k, 42)
     X = oracle.synth(nv, k, 4242).T  # k x nv

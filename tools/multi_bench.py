@@ -1,6 +1,8 @@
 """mvg_gemv_multi (several x per pass over A): every kernel variant against nv separate mvg_gemv
-calls (development tool). Prints one JSON line per (shape, nv, variant): time per call, the
-A-stream rate (8*M*K bytes / time) and the max relative error against rocBLAS (torch)."""
+calls (development tool). Prints one JSON line per (shape, nv, variant): time per call, the A-stream rate (8*M*K bytes / time) and the max relative error against rocBLAS (torch).
+
+    python tools/multi_bench.py [MxK,...|all] [variant-name-prefix,...]
+"""
 import json
 import os
 import sys
@@ -28,13 +30,12 @@ def timeit(fn, reps=10, rounds=5):
 
 
 def main():
-    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 and sys.argv[1] != "all" else None
+    vfilter = sys.argv[2].split(",") if len(sys.argv) > 2 else None  # variant name prefixes
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     nvar = lib.mvg_gemv_multi_variant_count()
-    for M, K in SHAPES:
-        if only and f"{M}x{K}" not in only:
-            continue
+    for M, K in [tuple(map(int, o.split("x"))) for o in only] if only else SHAPES:
         A = torch.empty(M, K, dtype=torch.float64, device=dev)
         check(lib.mvg_synth_fill_device(A.data_ptr(), K, M, K, 0, 0, K, 42, s), "fill")
         X = torch.rand(8, K, dtype=torch.float64, device=dev)
@@ -43,6 +44,8 @@ def main():
         for nv in (2, 4, 8):
             cands = [("separate", None)] + [(lib.mvg_gemv_multi_variant_name(v).decode(), v) for v in range(nvar)]
             for name, v in cands:
+                if vfilter and v is not None and not any(name.startswith(f) for f in vfilter):
+                    continue
                 if v is None:
                     def fn():
                         for j in range(nv):
