@@ -376,7 +376,7 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
 
 def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
     """mvg_gemv_multi (several x per pass over A; beyond the reference) on a
-    config-2-sized A: for nv = 2, 4, 8 the kernel's mean time (HIP events, `launches` back to
+    config-2-sized A: for nv = 2, 4, 8, 16 the kernel's mean time (HIP events, `launches` back to
     back), the rate at which it reads A and its algorithmic bytes (A once, every x and y), and
     the speed-up over nv separate mvg_gemv calls timed the same way. Each vector's y is checked
     against the single-vector kernel's (<= 1e-12)."""
@@ -386,7 +386,7 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
     from matvec_mpi_multiplier_amd._lib import check, lib
 
     s = torch.cuda.current_stream(local).cuda_stream
-    nvmax = 8
+    nvmax = 16
     dA, dX, dY, dy = mm.DeviceBuffer(M * K), mm.DeviceBuffer(K * nvmax), mm.DeviceBuffer(M * nvmax), mm.DeviceBuffer(M)
     try:
         check(lib.mvg_synth_fill_device(dA.ptr, K, M, K, 0, 0, K, 42, s), "fill A")
@@ -407,7 +407,7 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
         single = t(lambda: lib.mvg_gemv(dA.ptr, K, dX.ptr, dy.ptr, M, K, s))
         out = {"shape": [M, K], "single_ms": round(single, 5), "nv": {}}
         worst = 0.0
-        for nv in (2, 4, 8):
+        for nv in (2, 4, 8, 16):
             ms = t(lambda: lib.mvg_gemv_multi(dA.ptr, K, dX.ptr, K, dY.ptr, M, M, K, nv, s))
             Y = dY.download(M * nv).reshape(nv, M)
             for v in range(nv):
@@ -420,6 +420,7 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
                 "A_GBps": round(8 * M * K / (ms * 1e-3) / 1e9, 1),
                 "algorithmic_GBps": round(8 * (M * K + nv * (K + M)) / (ms * 1e-3) / 1e9, 1),
                 "speedup_vs_separate": round(nv * single / ms, 3),
+                "kernel": lib.mvg_gemv_multi_variant_name(lib.mvg_gemv_multi_auto_variant(K, K, M, K, nv)).decode(),
             }
         assert worst <= 1e-12, f"multi-vector y differs from the single-vector y by {worst}"
         out["max_rel_vs_single"] = worst

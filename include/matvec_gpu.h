@@ -162,7 +162,8 @@ const char* mvg_gemv_variant_name(int variant);
 
 /* Several x per pass over A (beyond the reference's surface):
  * Y[:, v] = A X[:, v] for v < nv, X k x nv and Y m x nv column-major (vector v at X + v*ldx,
- * Y + v*ldy; ldx >= k, ldy >= m). A is streamed once per group of 8 vectors, so the HBM cost
+ * Y + v*ldy; ldx >= k, ldy >= m). A is streamed once per group of 8 vectors (16 from 8192 rows
+ * of >= 1024 columns, on the matrix cores), so the HBM cost
  * of nv products approaches that of one. Same numerics contract as mvg_gemv. */
 int mvg_gemv_multi(const double* d_A, int64_t lda, const double* d_X, int64_t ldx, double* d_Y,
                    int64_t ldy, int64_t m, int64_t k, int nv, void* stream);
@@ -170,8 +171,9 @@ int mvg_gemv_multi(const double* d_A, int64_t lda, const double* d_X, int64_t ld
 int mvg_gemv_multi_variant(const double* d_A, int64_t lda, const double* d_X, int64_t ldx, double* d_Y,
                            int64_t ldy, int64_t m, int64_t k, int nv, int variant, void* stream);
 int mvg_gemv_multi_variant_count(void);
-/* the variant mvg_gemv_multi picks for each group of up to 8 of nv >= 2 vectors (16-B aligned A
- * and X, even lda and ldx); 0 for nv < 2 (the single-vector dispatch) */
+/* the variant mvg_gemv_multi picks for the first group of nv >= 2 vectors (16-B aligned A and X,
+ * even lda and ldx): up to 16 vectors per pass on long enough shapes, else up to 8; 0 for nv < 2
+ * (the single-vector dispatch) */
 int mvg_gemv_multi_auto_variant(int64_t lda, int64_t ldx, int64_t m, int64_t k, int nv);
 const char* mvg_gemv_multi_variant_name(int variant);
 

@@ -1420,10 +1420,168 @@ __global__ __launch_bounds__(NW * 64) void gemv_mdma(const double* __restrict__ 
     }
 }
 
-// host side of gemv_mdma's address limits: 16*RQ rows of A and NV rows of X in 32-bit offsets
-inline bool dma_ok(int rows_per_block, int64_t lda, int64_t ldx) {
+// Sixteen vectors per pass on the matrix cores: gemv_mdma's tiles and workgroup shape, with the
+// sums done by v_mfma_f64_16x16x4_f64 — a 16-row x 16-vector tile of Y per RQ row group, 4 f64
+// accumulators per lane instead of 16 x RQ, and one ds_read_b128 of x per step instead of one
+// per vector. fp64 MFMA has the fp64 VALU's peak on MI355X, so this pays only when all 16
+// columns carry vectors: nv = 9..16 in one pass over A instead of two.
+//   operands (step s, chunk c = 4s + g of the tile): lane (i = l & 15, g = l >> 4) holds row i's
+//            pair A[i][2c], A[i][2c+1] and lane (j = l & 15, g) vector j's pair x_j[2c], x_j[2c+1];
+//            the .x halves make one MFMA and the .y halves the next — k index g of each MFMA is
+//            column 8s + 2g (+1) for both operands, a fixed permutation of the tile's columns;
+//   x image: LDS slot (v, s) of the tile's x segment holds vector v's chunk s ^ (v & 15), the
+//            same XOR as A's rows, so the B reads are conflict-free too;
+//   result : lane (j, g) holds Y rows g + 4r (r < 4) of vector j in register r (gfx950's f64
+//            MFMA layout); the column tail (K % 2T) goes through the same MFMAs from global memory,
+//            4 columns a step, zero past K; partials meet in LDS in wave order.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int RQ, int T, int NB, int NW, int ROT>
+__global__ __launch_bounds__(NW * 64) void gemv_mdma16(const double* __restrict__ A, int64_t lda,
+                                                       const double* __restrict__ X, int64_t ldx,
+                                                       double* __restrict__ Y, int64_t ldy, int64_t M,
+                                                       int64_t K, int nv) {
+    static_assert(T == 16 || T == 32, "tile width: 16 or 32 chunks of 16 B");
+    constexpr int NV = 16;
+    constexpr int RB = 16 * RQ;
+    constexpr int kRows = 64 / T;
+    constexpr int kInst = RB / kRows;
+    constexpr int kXInst = NV * T / 64;
+    constexpr int kPer = kInst + kXInst;
+    static_assert(kPer * (NB - 1) <= 63, "loads in flight must fit the vmcnt counter");
+    constexpr int kCols = 2 * T;
+    constexpr int kRowBytes = 16 * T;
+    constexpr int kTileBytes = RB * kRowBytes;
+    constexpr int kBufBytes = kTileBytes + kXInst * 1024;
+    static_assert(NB * kBufBytes >= RQ * 4 * 64 * (int)sizeof(double), "partials fit the ring");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NW][NB * kBufBytes];
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * RB;
+    const int64_t ntiles = K / kCols;
+    unsigned char* const ring = lds[w];
+
+    uint32_t aoff[kInst], xoff[kXInst];
+#pragma unroll
+    for (int j = 0; j < kInst; ++j) {
+        const int row = j * kRows + lane / T;
+        const int64_t rr = r0 + row < M ? row : M - 1 - r0;
+        aoff[j] = (uint32_t)((rr * lda + 2 * ((lane % T) ^ (row & 15))) * (int64_t)sizeof(double));
+    }
+#pragma unroll
+    for (int j = 0; j < kXInst; ++j) {
+        const int q = 64 * j + lane;  // LDS slot: vector q / T, slot q % T
+        const int v = q / T;
+        const int c = (q % T) ^ (v & 15);
+        xoff[j] = (uint32_t)(((v < nv ? v : 0) * ldx + 2 * c) * (int64_t)sizeof(double));
+    }
+    const unsigned char* const a0 = reinterpret_cast<const unsigned char*>(A + r0 * lda);
+    const unsigned char* const x0 = reinterpret_cast<const unsigned char*>(X);
+    const int64_t rot = ROT > 0 && ntiles > 0 ? ((int64_t)blockIdx.x * ROT) % ntiles : 0;
+    auto issue = [&](int64_t t, int b) {
+        t += rot;
+        if (t >= ntiles) t -= ntiles;
+        const int64_t colb = t * kCols * (int64_t)sizeof(double);
+        unsigned char* buf = ring + b * kBufBytes;
+#pragma unroll
+        for (int j = 0; j < kInst; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(a0 + colb + aoff[j]), (lds_void_t)(buf + j * 1024),
+                                             16, 0, 2 /* nt */);
+#pragma unroll
+        for (int j = 0; j < kXInst; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void_t)(x0 + colb + xoff[j]),
+                                             (lds_void_t)(buf + kTileBytes + j * 1024), 16, 0, 0);
+    };
+
+    const int i = lane & 15;  // A row / x vector of this lane's operands
+    const int g = lane >> 4;  // k index
+    dbl4 acc[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    auto consume = [&](int b) {
+        const unsigned char* buf = ring + b * kBufBytes;
+#pragma unroll
+        for (int s = 0; s < T / 4; ++s) {
+            const int c = 4 * s + g;
+            const uint32_t sw = 16 * (uint32_t)(c ^ i);
+            const dbl2 xb = *reinterpret_cast<const dbl2*>(buf + kTileBytes + i * kRowBytes + sw);
+#pragma unroll
+            for (int q = 0; q < RQ; ++q) {
+                const dbl2 a = *reinterpret_cast<const dbl2*>(buf + (i + 16 * q) * kRowBytes + sw);
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, xb.x, acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, xb.y, acc[q], 0, 0, 0);
+            }
+        }
+    };
+
+    const int64_t nt = ntiles > w ? (ntiles - w + NW - 1) / NW : 0;
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p)
+        if (p < nt) issue(w + (int64_t)NW * p, p);
+    for (int64_t u = 0; u < nt; ++u) {
+        const int64_t un = u + NB - 1;
+        if (un < nt) {
+            wait_lgkmcnt0();
+            issue(w + (int64_t)NW * un, (int)(un % NB));
+            wait_vmcnt<kPer*(NB - 1)>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        consume((int)(u % NB));
+    }
+
+    // column tail through the same MFMAs: 4 columns a step (k index g), zero past K
+    {
+        const double* xj = X + (i < nv ? i : 0) * ldx;
+        for (int64_t c0 = ntiles * kCols + 4 * w; c0 < K; c0 += 4 * NW) {
+            const int64_t c = c0 + g;
+            const double xv = c < K ? xj[c] : 0.0;
+#pragma unroll
+            for (int q = 0; q < RQ; ++q) {
+                const int64_t rr = r0 + i + 16 * q < M ? r0 + i + 16 * q : M - 1;
+                const double a = c < K ? A[rr * lda + c] : 0.0;
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xv, acc[q], 0, 0, 0);
+            }
+        }
+    }
+
+    // lane (j, g) register r: Y row 16q + g + 4r of vector j
+    if constexpr (NW == 1) {
+#pragma unroll
+        for (int q = 0; q < RQ; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = r0 + 16 * q + g + 4 * r;
+                if (row < M && i < nv) Y[i * ldy + row] = acc[q][r];
+            }
+    } else {
+        wait_vmcnt<0>();
+        wait_lgkmcnt0();
+        double* part = reinterpret_cast<double*>(ring);
+#pragma unroll
+        for (int q = 0; q < RQ; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[(q * 4 + r) * 64 + lane] = acc[q][r];
+        __syncthreads();
+        for (int t = threadIdx.x; t < RQ * 4 * 64; t += NW * 64) {
+            const int l = t % 64, r = (t / 64) % 4, q = t / 256;
+            const int64_t row = r0 + 16 * q + (l >> 4) + 4 * r;
+            if (row < M && (l & 15) < nv) {
+                double s = 0.0;
+#pragma unroll
+                for (int ww = 0; ww < NW; ++ww) s += reinterpret_cast<const double*>(lds[ww])[t];
+                Y[(l & 15) * ldy + row] = s;
+            }
+        }
+    }
+}
+
+// host side of the DMA forms' address limits: rows_per_block rows of A and nvec rows of X in
+// 32-bit offsets
+inline bool dma_ok(int rows_per_block, int64_t lda, int64_t ldx, int nvec = 8) {
     return (int64_t)rows_per_block * lda * (int64_t)sizeof(double) < (1ll << 31) &&
-           8 * ldx * (int64_t)sizeof(double) < (1ll << 31);
+           nvec * ldx * (int64_t)sizeof(double) < (1ll << 31);
 }
 
 typedef void (*gemv_multi_fn)(const double*, int64_t, const double*, int64_t, double*, int64_t, int64_t,
@@ -1434,7 +1592,8 @@ struct MultiVariant {
     gemv_multi_fn fn[3];  // NV = 2, 4, 8
     int rows_per_block;
     int block;
-    bool dma = false;     // gemv_mdma: 32-bit DMA offsets (dma_ok)
+    bool dma = false;     // gemv_mdma / gemv_mdma16: 32-bit DMA offsets (dma_ok)
+    gemv_multi_fn fn16 = nullptr;  // gemv_mdma16: up to 16 vectors per pass (fn[] unused)
 };
 
 #define MVEC(LPR, RPG, UNR)                                                                              \
@@ -1464,6 +1623,10 @@ struct MultiVariant {
      {gemv_mdma<RQ, T, NB, NW, 2, ROT>, gemv_mdma<RQ, T, NB, NW, 4, ROT>,                                \
       gemv_mdma<RQ, T, NB, NW, 8, ROT>},                                                                 \
      16 * RQ, NW * 64, true}
+
+#define M16(RQ, T, NB, NW, ROT)                                                                          \
+    {"m16_r" #RQ "_t" #T "_b" #NB "_w" #NW "_s" #ROT, {nullptr, nullptr, nullptr}, 16 * RQ, NW * 64, true, \
+     gemv_mdma16<RQ, T, NB, NW, ROT>}
 
 static constexpr MultiVariant kMultiVariants[] = {
     {"auto", {nullptr, nullptr, nullptr}, 0, 0},  // 0
@@ -1516,6 +1679,14 @@ static constexpr MultiVariant kMultiVariants[] = {
     MDMAS(2, 16, 4, 2, 5),                        // 47
     MDMAS(1, 16, 3, 2, 5),                        // 48
     MDMAS(4, 16, 2, 1, 5),                        // 49
+    M16(2, 16, 2, 4, 5),                          // 50 16 vectors per pass, matrix cores
+    M16(2, 16, 2, 2, 5),                          // 51
+    M16(2, 16, 3, 2, 5),                          // 52
+    M16(4, 16, 2, 2, 5),                          // 53
+    M16(4, 16, 2, 1, 5),                          // 54
+    M16(1, 16, 2, 4, 5),                          // 55
+    M16(2, 32, 2, 2, 5),                          // 56
+    M16(1, 16, 3, 4, 5),                          // 57
 };
 constexpr int kNumMultiVariants = (int)(sizeof(kMultiVariants) / sizeof(kMultiVariants[0]));
 
@@ -1550,6 +1721,15 @@ static_assert(kMd2w4s5 > 0 && kMd1w4s5 > 0, "multi-vector dispatch names a missi
 int pick_multi_dma(int64_t m, int64_t k, int nvp) {
     if (m >= 8192) return (nvp >= 8 ? k >= 1024 : nvp >= 4 ? k >= 1280 : k >= 6144) ? kMd2w4s5 : 0;
     return m >= 4096 && k >= 8192 ? kMd1w4s5 : 0;
+}
+
+// 9..16 vectors: one pass on the matrix cores (gemv_mdma16) where the DMA forms run, else two
+// passes of <= 8
+constexpr int kM16 = variant_id(kMultiVariants, "m16_r2_t16_b2_w4_s5");
+static_assert(kM16 > 0, "multi-vector dispatch names a missing 16-vector variant");
+
+int pick_multi16(int64_t m, int64_t k, int64_t lda, int64_t ldx) {
+    return m >= 8192 && k >= 1024 && dma_ok(kMultiVariants[kM16].rows_per_block, lda, ldx, 16) ? kM16 : 0;
 }
 
 int pick_multi_variant(int64_t m, int64_t k, int nvp, int64_t lda, int64_t ldx) {
@@ -1654,6 +1834,10 @@ int mvg_gemv_multi_variant_count(void) { return kNumMultiVariants; }
 
 int mvg_gemv_multi_auto_variant(int64_t lda, int64_t ldx, int64_t m, int64_t k, int nv) {
     if (nv < 2) return 0;
+    if (nv > 8) {
+        const int v = pick_multi16(m, k, lda, ldx);
+        if (v > 0) return v;
+    }
     const int g = nv < 8 ? nv : 8;
     return pick_multi_variant(m, k, g <= 2 ? 2 : g <= 4 ? 4 : 8, lda, ldx);
 }
@@ -1681,27 +1865,38 @@ int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_
         }
         return MVG_OK;
     }
-    for (int v0 = 0; v0 < nv; v0 += 8) {  // groups of <= 8 vectors per pass over A
-        const int g = nv - v0 < 8 ? nv - v0 : 8;
+    const bool fixed16 = variant != 0 && kMultiVariants[variant].fn16 != nullptr;
+    for (int v0 = 0; v0 < nv;) {  // groups of <= 8 (or 16) vectors per pass over A
+        const int rest = nv - v0;
+        int v = variant, g = rest < 8 ? rest : 8;
+        if (fixed16) {
+            g = rest < 16 ? rest : 16;
+        } else if (variant == 0 && rest > 8 && (v = pick_multi16(m, k, lda, ldx)) > 0) {
+            g = rest < 16 ? rest : 16;  // 9..16 vectors: one pass on the matrix cores
+        } else {
+            v = variant;
+        }
         const double* Xg = X + v0 * ldx;
         double* Yg = Y + v0 * ldy;
-        if (g == 1 && variant == 0) {  // one vector: the single-vector dispatch
+        v0 += g;
+        if (g == 1 && v == 0) {  // one vector: the single-vector dispatch
             int rc = mvg_gemv_variant(A, lda, Xg, Yg, m, k, 0, stream);
             if (rc != MVG_OK) return rc;
             continue;
         }
         const int slot = g <= 2 ? 0 : g <= 4 ? 1 : 2;
-        const int v = variant ? variant : pick_multi_variant(m, k, 2 << slot, lda, ldx);
+        if (v == 0) v = pick_multi_variant(m, k, 2 << slot, lda, ldx);
         const MultiVariant& mv = kMultiVariants[v];
-        if (mv.dma && !dma_ok(mv.rows_per_block, lda, ldx))
+        if (mv.dma && !dma_ok(mv.rows_per_block, lda, ldx, mv.fn16 ? 16 : 8))
             return fail(MVG_E_INVALID, "mvg_gemv_multi: lda or ldx too large for the DMA variant");
+        const gemv_multi_fn fn = mv.fn16 ? mv.fn16 : mv.fn[slot];
         // launches of < 2^32 threads each (the grid-size cap), row ranges in order
         const int64_t max_rows = ((1ll << 31) / mv.block) * mv.rows_per_block;
         for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
             const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
             const int64_t blocks = (mm + mv.rows_per_block - 1) / mv.rows_per_block;
-            hipLaunchKernelGGL(mv.fn[slot], dim3((unsigned)blocks), dim3(mv.block), 0, s, A + r0 * lda, lda, Xg,
-                               ldx, Yg + r0, ldy, mm, k, g);
+            hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(mv.block), 0, s, A + r0 * lda, lda, Xg, ldx,
+                               Yg + r0, ldy, mm, k, g);
             MVG_HIP(hipGetLastError());
         }
     }

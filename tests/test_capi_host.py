@@ -441,3 +441,6 @@ def test_multi_vector_dispatch_takes_dma_forms_on_long_rows():
     assert not name(4194304, 512, 8).startswith("mdma")      # short rows: x resident in LDS
     assert not name(16384, 16384, 8, lda=1 << 24).startswith("mdma")
     assert lib.mvg_gemv_multi_auto_variant(16384, 16384, 16384, 16384, 1) == 0
+    # 9..16 vectors: one pass on the matrix cores where the DMA forms run
+    assert name(16384, 16384, 16) == name(8192, 1024, 9) == "m16_r2_t16_b2_w4_s5"
+    assert not name(4200, 4200, 16).startswith("m16")

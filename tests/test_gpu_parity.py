@@ -320,7 +320,7 @@ def test_engine_multiply_before_inputs_is_state_error(comm1):
                                     (100, 3000, 11), (50, 1001, 4),
                                     # the automatic DMA forms, with row and tile tails
                                     (8195, 1030, 8), (8200, 1290, 3), (8197, 6150, 2), (4099, 8194, 6),
-                                    (8192, 1024, 16)])
+                                    (8192, 1024, 16), (8203, 1058, 13), (8193, 2050, 25)])
 def test_multi_vector_gemv(m, k, nv):
     A = oracle.synth(m, k, 42)
     X = oracle.synth(nv, k, 4242).T  # k x nv
@@ -353,6 +353,35 @@ def test_multi_vector_every_variant(m, k, nv):
             for v in range(nv):
                 assert max_rel(Y[v], want[v]) <= TOL, (name, v)
             assert np.isnan(Y[nv:]).all(), name
+    finally:
+        for b in (dA, dX, dY):
+            b.free()
+
+
+@pytest.mark.parametrize("m,k,nv", [(257, 1000, 16), (33, 6002, 11), (130, 4226, 9), (77, 256, 16), (9, 130, 12),
+                                    (4099, 64, 16), (1000, 512, 3)])
+def test_multi_vector_16_per_pass_every_variant(m, k, nv):
+    """The 16-vector matrix-core variants (gemv_mdma16) on every shape class: row tails, tile
+    tails (K not a multiple of a tile), K shorter than a tile, vectors past nv never written."""
+    from matvec_mpi_multiplier_amd._lib import check, lib
+
+    A = oracle.synth(m, k, 42)
+    X = oracle.synth(nv, k, 4242)
+    want = [oracle.multiply_std_rowwise(A, np.ascontiguousarray(X[v])) for v in range(nv)]
+    dA, dX = mm.DeviceBuffer(m * k).upload(A), mm.DeviceBuffer(nv * k).upload(X)
+    dY = mm.DeviceBuffer(m * 16)
+    try:
+        names = [lib.mvg_gemv_multi_variant_name(v).decode() for v in range(lib.mvg_gemv_multi_variant_count())]
+        m16 = [v for v, n in enumerate(names) if n.startswith("m16_")]
+        assert m16
+        for var in m16:
+            dY.upload(np.full(m * 16, np.nan))
+            check(lib.mvg_gemv_multi_variant(dA.ptr, k, dX.ptr, k, dY.ptr, m, m, k, nv, var, None), names[var])
+            check(lib.mvg_stream_sync(None), "sync")
+            Y = dY.download(m * 16).reshape(16, m)
+            for v in range(nv):
+                assert max_rel(Y[v], want[v]) <= TOL, (names[var], v)
+            assert np.isnan(Y[nv:]).all(), names[var]
     finally:
         for b in (dA, dX, dY):
             b.free()

@@ -38,10 +38,10 @@ def main():
     for M, K in [tuple(map(int, o.split("x"))) for o in only] if only else SHAPES:
         A = torch.empty(M, K, dtype=torch.float64, device=dev)
         check(lib.mvg_synth_fill_device(A.data_ptr(), K, M, K, 0, 0, K, 42, s), "fill")
-        X = torch.rand(8, K, dtype=torch.float64, device=dev)
-        Y = torch.empty(8, M, dtype=torch.float64, device=dev)
+        X = torch.rand(16, K, dtype=torch.float64, device=dev)
+        Y = torch.empty(16, M, dtype=torch.float64, device=dev)
         ref = X @ A.T  # rocBLAS
-        for nv in (2, 4, 8):
+        for nv in (2, 4, 8, 16):
             cands = [("separate", None)] + [(lib.mvg_gemv_multi_variant_name(v).decode(), v) for v in range(nvar)]
             for name, v in cands:
                 if vfilter and v is not None and not any(name.startswith(f) for f in vfilter):
