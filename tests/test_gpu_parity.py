@@ -3,8 +3,10 @@
 Bar (BASELINE.json north_star): <= 1e-12 relative per element against the reference on the
 same inputs — the GPU sums in a different (fixed) order than the reference's sequential
 loop. Checked against (a) the golden vectors the real reference produced, (b) the pinned
-oracle on the same seeded inputs, and (c) at the full BASELINE sizes through sampled rows
-plus size-independent properties (exact scaling by 2, run-to-run bit determinism).
+oracle on the same seeded inputs, and (c) at the full BASELINE sizes: every row of y at
+configs 2, 3 and 5 whole and config 4's per-GPU block against the oracle (tree within the bar,
+exact bit for bit), sampled rows up to config 4 whole (128 GiB), and size-independent
+properties (exact scaling by 2, run-to-run bit determinism).
 """
 import os
 
@@ -263,6 +265,38 @@ def test_full_size_sampled_rows_and_properties(comm1, alg, R, Cn):
     # checksum: sum(y) = sum_j x_j * colsum_j is too costly here; instead every y_i lies in
     # [0, C * 0.9999^2] for inputs in [0, 0.9999]
     assert y1.min() >= 0 and y1.max() <= Cn * 0.9999 * 0.9999
+
+
+@pytest.mark.parametrize("alg,R,Cn", [
+    ("rowwise", 16384, 16384),     # config 2
+    ("rowwise", 524288, 512),      # config 5's per-GPU shard
+    ("colwise", 65536, 8192),      # config 3's per-GPU strip shape (65536^2 over 8 GPUs)
+    ("blockwise", 65536, 32768),   # config 4's per-GPU block (131072^2 on a 2 x 4 grid)
+    ("rowwise", 4194304, 512),     # config 5 whole on one GPU (16 GiB)
+    ("colwise", 65536, 65536),     # config 3 whole on one GPU (32 GiB)
+])
+def test_full_size_whole_y_against_oracle(comm1, alg, R, Cn):
+    """Every row of y at the BASELINE configs' per-GPU shapes against the oracle's sequential
+    sums: tree mode within TOL, exact mode bit for bit — on the row-major kernels (first
+    multiply) and on the engine's column-panel copy where it builds one (second multiply). At
+    P = 1 each multiplier's y is multiply_std_rowwise's: a one-strip column split scales in place
+    and sums from 0.0 (multiplier_colwise.c:107-122), a 1 x 1 grid adds its one partial to 0
+    (multiplier_blockwise.c:206) — the golden vectors pin that at P = 1."""
+    A = oracle.synth(R, Cn, 42)
+    want = oracle.multiply_std_rowwise(A, oracle.synth(1, Cn, 4242)[0])
+    del A
+    with mm.Multiplier(alg, R, Cn, comm1) as e:
+        e.fill_synth()
+        e.multiply()
+        y = e.collect()
+        e.set_exact(True)
+        e.multiply()
+        y_rm = e.collect()
+        e.multiply()
+        y_2 = e.collect()
+    assert max_rel(y, want) <= TOL
+    np.testing.assert_array_equal(y_rm, want)
+    np.testing.assert_array_equal(y_2, want)
 
 
 def test_scaling_x_by_two_is_exact():
