@@ -491,7 +491,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         if (l.rank == 0)
             if ((rc = alloc_doubles(&s.dy, R)) != MVG_OK) return bail(rc);
         // Warm the device before any timed loop: first-touch every buffer (the first H2D into
-        // never-touched HBM ran at 11 GB/s instead of 56, tools/numa_h2d.py) and launch the
+        // never-touched HBM ran at 11 GB/s instead of 56, tools/probes/numa_h2d.py) and launch the
         // shard's GEMV once (loads its code object and any split-K workspace). These one-time
         // costs are the GPU runtime's analogue of MPI_Init; without this they landed in the
         // executables' first timed iteration (+0.1 ms on the mean at 600 x 600).
@@ -509,7 +509,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         // ... and one page-locked H2D into A's buffer and D2H out of y's, as large as those
         // transfers will be up to 4 MiB, on each stream that distributes or collects. The
         // runtime brings its large-copy path up on the first such transfer of the process:
-        // 8.2 ms once (tools/first_copy.py: 2.88 MB from any page-locked buffer, 8.2 ms first,
+        // 8.2 ms once (tools/probes/first_copy.py: 2.88 MB from any page-locked buffer, 8.2 ms first,
         // 66 us after; 512-B copies do not trigger it), which otherwise landed in the
         // executables' first timed iteration (bin/multiplier_rowwise 600 600, MVG_ITER_LOG).
         const int64_t a_elems = std::min<int64_t>(p.n_rows * p.n_cols, 1 << 19);

@@ -4,9 +4,9 @@ Bar (BASELINE.json north_star): <= 1e-12 relative per element against the refere
 same inputs — the GPU sums in a different (fixed) order than the reference's sequential
 loop. Checked against (a) the golden vectors the real reference produced, (b) the pinned
 oracle on the same seeded inputs, and (c) at the full BASELINE sizes: every row of y at
-configs 2, 3 and 5 whole and config 4's per-GPU block against the oracle (tree within the bar,
-exact bit for bit), sampled rows up to config 4 whole (128 GiB), and size-independent
-properties (exact scaling by 2, run-to-run bit determinism).
+configs 2, 3, 4 and 5 whole (config 4: 128 GiB on one GPU) and at their per-GPU shards against
+the oracle (tree within the bar, exact bit for bit), plus size-independent properties (exact
+scaling by 2, run-to-run bit determinism).
 """
 import os
 
@@ -267,6 +267,25 @@ def test_full_size_sampled_rows_and_properties(comm1, alg, R, Cn):
     assert y1.min() >= 0 and y1.max() <= Cn * 0.9999 * 0.9999
 
 
+def _oracle_y_by_row_blocks(R, Cn, block_bytes=256 << 20):
+    """The oracle's y = multiply_std_rowwise(A, x) of the synthetic A (seed 42) and x (4242),
+    generated and summed in row blocks on the host's allowed CPUs (ctypes releases the GIL), so
+    config 4's 128 GiB A is never held whole."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    x = oracle.synth(1, Cn, 4242)[0]
+    y = np.empty(R)
+    rows = max(1, block_bytes // (8 * Cn))
+
+    def block(r0):
+        nr = min(rows, R - r0)
+        y[r0:r0 + nr] = oracle.multiply_std_rowwise(oracle.synth_block(r0, nr, 0, Cn, Cn, 42), x)
+
+    with ThreadPoolExecutor(max_workers=max(1, min(16, len(os.sched_getaffinity(0))))) as ex:
+        list(ex.map(block, range(0, R, rows)))
+    return y
+
+
 @pytest.mark.parametrize("alg,R,Cn", [
     ("rowwise", 16384, 16384),     # config 2
     ("rowwise", 524288, 512),      # config 5's per-GPU shard
@@ -274,6 +293,7 @@ def test_full_size_sampled_rows_and_properties(comm1, alg, R, Cn):
     ("blockwise", 65536, 32768),   # config 4's per-GPU block (131072^2 on a 2 x 4 grid)
     ("rowwise", 4194304, 512),     # config 5 whole on one GPU (16 GiB)
     ("colwise", 65536, 65536),     # config 3 whole on one GPU (32 GiB)
+    ("blockwise", 131072, 131072),  # config 4 whole on one GPU (1 x 1 grid, 128 GiB)
 ])
 def test_full_size_whole_y_against_oracle(comm1, alg, R, Cn):
     """Every row of y at the BASELINE configs' per-GPU shapes against the oracle's sequential
@@ -282,9 +302,7 @@ def test_full_size_whole_y_against_oracle(comm1, alg, R, Cn):
     P = 1 each multiplier's y is multiply_std_rowwise's: a one-strip column split scales in place
     and sums from 0.0 (multiplier_colwise.c:107-122), a 1 x 1 grid adds its one partial to 0
     (multiplier_blockwise.c:206) — the golden vectors pin that at P = 1."""
-    A = oracle.synth(R, Cn, 42)
-    want = oracle.multiply_std_rowwise(A, oracle.synth(1, Cn, 4242)[0])
-    del A
+    want = _oracle_y_by_row_blocks(R, Cn)
     with mm.Multiplier(alg, R, Cn, comm1) as e:
         e.fill_synth()
         e.multiply()

@@ -2,7 +2,7 @@
 read-only stream kernel on several freshly allocated 2 GiB buffers of one process, to tell
 allocation placement effects (spread across buffers) from box effects (spread across runs).
 
-    python tools/alloc_spread.py [--buffers 8]
+    python tools/probes/alloc_spread.py [--buffers 8]
 """
 import argparse
 import json
@@ -11,7 +11,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 
 

@@ -1,6 +1,6 @@
 """Where does the row-major exact GEMV lose time inside the engine? (development tool, one MI355X)
 
-    python tools/engine_exact_probe.py [M] [K] [launches]
+    python tools/probes/engine_exact_probe.py [M] [K] [launches]
 
 The same kernels (mvg_gemv tree, mvg_gemv_exact) on the same shape, three ways, interleaved twice:
   engine : mm.Multiplier (fill_synth, MVG_NO_PANELS=1), kernel time from its HIP events;
@@ -15,7 +15,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 os.environ["MVG_NO_PANELS"] = "1"
 from matvec_mpi_multiplier_amd import multiplier as mm  # noqa: E402
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402

@@ -2,7 +2,7 @@
 tool) Times the tree GEMV and two exact variants at 16384^2 on an A allocated first in the
 process, then on an A allocated after a 40 GiB spacer, then again on the first A.
 
-    python tools/exact_alloc_probe.py [rounds]
+    python tools/probes/exact_alloc_probe.py [rounds]
 """
 import json
 import os
@@ -10,7 +10,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 
 

@@ -12,7 +12,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd._lib import lib, check  # noqa: E402
 
 hip = C.CDLL("libamdhip64.so")

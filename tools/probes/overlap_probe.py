@@ -1,7 +1,7 @@
 """End-to-end time (root's host A, x -> distribute -> multiply -> y on the host) with the
 chunked distribution (mvg_engine_set_overlap) at several chunk counts, one GPU (development tool).
 
-    python tools/overlap_probe.py [R] [C] [iters]
+    python tools/probes/overlap_probe.py [R] [C] [iters]
 """
 import json
 import os
@@ -10,7 +10,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd import multiplier as mm  # noqa: E402
 from matvec_mpi_multiplier_amd._lib import lib  # noqa: E402
 

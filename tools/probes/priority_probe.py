@@ -1,9 +1,9 @@
 """The row-major exact GEMV (and the tree one) on streams of different priority and on several
 fresh streams of each, in one process (development tool, one MI355X).
 
-    python tools/priority_probe.py [M] [K] [launches]
+    python tools/probes/priority_probe.py [M] [K] [launches]
 
-tools/queue_probe.py showed the exact kernel's time moving by up to 10 % with the hardware queue
+tools/probes/queue_probe.py showed the exact kernel's time moving by up to 10 % with the hardware queue
 its stream lands on; this asks whether a stream's priority (hipStreamCreateWithPriority through
 torch.cuda.Stream(priority=...)) pins it. One JSON object per (priority, stream index).
 """
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 
 

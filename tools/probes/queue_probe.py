@@ -1,7 +1,7 @@
 """Does the number of HIP streams (hardware queues) a process holds slow the exact GEMV down?
 (development tool, one MI355X)
 
-    python tools/queue_probe.py [M] [K] [launches]
+    python tools/probes/queue_probe.py [M] [K] [launches]
 
 Times mvg_gemv (tree) and mvg_gemv_exact on one torch-allocated A, on torch's current stream,
 as the process adds HIP streams: none; 1, 2, 3 and 6 more streams that each ran one tiny kernel
@@ -15,7 +15,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd import multiplier as mm  # noqa: E402
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 

@@ -3,7 +3,7 @@
 (tools/micro/seq_read.hip, several grid sizes and load depths), per-wave contiguous ranges, and
 the product's mvg_stream_read — to place the GEMV against the best read rate the chip gives.
 
-    python tools/read_calibration.py [rounds] [M,K ...]
+    python tools/probes/read_calibration.py [rounds] [M,K ...]
 
 One JSON object per (shape, kernel): median / min microseconds over interleaved rounds of 10
 launches, and GB/s of the A bytes (reads of x and writes of y excluded for the read kernels;
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 

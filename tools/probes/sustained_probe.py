@@ -1,7 +1,7 @@
 """Per-launch time of the tree GEMV, the row-major exact GEMV and the exact GEMV over column
 panels as a function of how many launches run back to back (development tool, one MI355X).
 
-    python tools/sustained_probe.py [M] [K] [rounds]
+    python tools/probes/sustained_probe.py [M] [K] [rounds]
 
 Short bursts (the variant sweeps: 10 launches per timing) and long runs (the bench: hundreds of
 multiplies in a row) can see different rates when a kernel's power draw lowers the sustained
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 
 

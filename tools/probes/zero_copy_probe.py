@@ -1,7 +1,7 @@
 """Zero-copy probe (development tool): can the GEMV read the root's page-locked host A directly
 over PCIe faster than the engine's H2D copy + GEMV on the copy?
 
-    python tools/zero_copy_probe.py [--iters 50]
+    python tools/probes/zero_copy_probe.py [--iters 50]
 
 Per size, host-timed medians (stream synchronize at the end of each iteration):
   copy : H2D of A and x (DMA) -> GEMV on the device copy -> D2H of y   (the engine's e2e form)
@@ -18,7 +18,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 
 
