@@ -3,10 +3,12 @@
 # device-resident shape, one pass per counter group (rocprofv3 does not split groups over passes),
 # each pass under its own hard time limit. Development tool (MI355X box).
 #   tools/pmc_passes.sh OUTDIR M K VARIANT [VARIANT ...]
-# VARIANT: an mvg_gemv_exact_variant_name, "auto" or "panels" (tools/exact_probe.py). Each pass
-# lands in OUTDIR/<variant>/<group>/; summarise with tools/pmc_traffic.py.
+# VARIANT: an mvg_gemv_exact_variant_name, "auto" or "panels" (tools/exact_probe.py), or with
+# PMC_PROBE=tools/multi_probe.py a vector count "nv<N>" (mvg_gemv_multi). Each pass lands in
+# OUTDIR/<variant>/<group>/; summarise with tools/pmc_traffic.py.
 set -euo pipefail
 OUT="$1"; M="$2"; K="$3"; shift 3
+PROBE="${PMC_PROBE:-tools/exact_probe.py}"
 PASSES=(
   "fetch:FETCH_SIZE"
   "write:WRITE_SIZE"
@@ -20,7 +22,7 @@ for v in "$@"; do
     mkdir -p "$OUT/$v/$name"
     # shellcheck disable=SC2086
     timeout -s KILL 90 rocprofv3 --pmc $counters --output-format csv -d "$OUT/$v/$name" \
-        -- python3 tools/exact_probe.py "$M" "$K" 10 "$v" > "$OUT/$v/$name/run.log" 2>&1
+        -- python3 "$PROBE" "$M" "$K" 10 "$v" > "$OUT/$v/$name/run.log" 2>&1
     echo "pmc $v $name done"
   done
 done
