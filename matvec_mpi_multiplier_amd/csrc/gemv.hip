@@ -789,6 +789,7 @@ static int64_t split_count(const Variant& var, int64_t M, int64_t K, bool force)
 
 // HIP caps a launch at gridDim.x * blockDim.x < 2^32 threads: very tall problems run as
 // several launches over consecutive row ranges (each range is an independent GEMV).
+constexpr int64_t kOneRowLaunchBytes = 1ll << 30;
 static int launch(int v, const double* A, int64_t lda, const double* x, double* y, int64_t M,
                   int64_t K, hipStream_t s, bool force_split) {
     const Variant& var = kVariants[v];
@@ -810,7 +811,17 @@ static int launch(int v, const double* A, int64_t lda, const double* x, double* 
         MVG_HIP(hipGetLastError());
         return MVG_OK;
     }
-    const int64_t max_rows = max_blocks * var.rows_per_block;
+    int64_t max_rows = max_blocks * var.rows_per_block;
+    // One row per wave (short rows): at most 1 GiB of A per launch. A longer launch of this
+    // form streams at one of two rates from process to process (config 5's 16 GiB: 2.36-2.38 ms
+    // or 2.50-2.53 ms, the slow one in most processes); 1 GiB launches run at 2.35-2.36 ms in the
+    // slow case, 2.39-2.40 (the extra launch boundaries) in the fast one, and the 2 GiB shard at
+    // 292 instead of 301-310 us (round 3, profiles/r03/sublaunch/).
+    if (v == kVecOneRow) {
+        int64_t cap = (kOneRowLaunchBytes / (lda * (int64_t)sizeof(double))) / var.rows_per_block * var.rows_per_block;
+        if (cap < var.rows_per_block) cap = var.rows_per_block;
+        if (cap < max_rows) max_rows = cap;
+    }
     for (int64_t r0 = 0; r0 < M; r0 += max_rows) {
         const int64_t m = M - r0 < max_rows ? M - r0 : max_rows;
         // row-pair forms: a last block of 2p rows with r < 2p rows left needs min(p, r) pairs,

@@ -787,6 +787,9 @@ constexpr int kPanelRows = seq_id(kPanelVariants, "panel_l8_w2_u8");
 static_assert(kPanelRows > 0, "panel dispatch names a missing variant");
 constexpr int64_t kPanelWidth = 256;
 
+constexpr int64_t kShortRowK = 768;
+constexpr int64_t kShortRowLaunchBytes = 1ll << 30;
+
 // one form for every shape: 24 segments in flight gained only 1-2 % from 32768 rows (round 2),
 // inside the box-to-box spread, so round 3 dropped that threshold
 static int pick_panel_variant(int64_t) { return kPanelRows; }
@@ -831,7 +834,15 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
     if (var.xlds && k > kXlMaxK) return fail(MVG_E_INVALID, "mvg_gemv_exact: x-in-LDS variant needs k <= 8192");
     // k == 0 runs the kernel too: every row's sum stays 0 (the reference's `sum = 0`)
     // grid-size cap: fewer than 2^32 threads per launch
-    const int64_t max_rows = ((1ll << 32) / (64 * var.waves) - 1) * var.rows;
+    int64_t max_rows = ((1ll << 32) / (64 * var.waves) - 1) * var.rows;
+    // short rows (K <= 768): at most 1 GiB of A per launch, as the tree form's one-row waves
+    // (gemv.hip): config 5's 16 GiB in 2.46 ms instead of 2.58, its 2 GiB shard 316 against
+    // 318 us (round 3, profiles/r03/sublaunch/)
+    if (k > 0 && k <= kShortRowK) {  // (k > 0: then lda >= k >= 1)
+        int64_t cap = kShortRowLaunchBytes / (lda * (int64_t)sizeof(double)) / var.rows * var.rows;
+        if (cap < var.rows) cap = var.rows;
+        if (cap < max_rows) max_rows = cap;
+    }
     const size_t lds = var.xlds ? (size_t)k * sizeof(double) : 0;
     for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
         const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
