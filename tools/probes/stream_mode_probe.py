@@ -34,6 +34,7 @@ def timed(fn, stream, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", type=int, default=6)
+    ap.add_argument("--buffers", type=int, default=1, help="more 16 GiB buffers, each timed on the default stream")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     M, K = 4194304, 512
@@ -55,6 +56,21 @@ def main():
             ta = timed(lambda: lib.mvg_gemv(a, K, xp, yp, M, K, h), st)
             print(json.dumps({"round": rnd, "stream": i, "one_launch_us": round(t1 * 1e3, 1),
                               "dispatch_1GiB_launches_us": round(ta * 1e3, 1)}), flush=True)
+    # the same on further buffers (placement) in this process, default stream
+    bufs = [A]
+    for b in range(1, args.buffers):
+        B = torch.empty(M * K, dtype=torch.float64, device=dev)
+        check(lib.mvg_synth_fill_device(B.data_ptr(), K, M, K, 0, 0, K, 42, s0.cuda_stream), "fill B")
+        bufs.append(B)
+    torch.cuda.synchronize()
+    for rnd in range(2):
+        for b, B in enumerate(bufs):
+            p, h = B.data_ptr(), s0.cuda_stream
+            t1 = timed(lambda: lib.mvg_gemv_variant(p, K, xp, yp, M, K, one, h), s0)
+            ta = timed(lambda: lib.mvg_gemv(p, K, xp, yp, M, K, h), s0)
+            print(json.dumps({"round": rnd, "buffer": b, "addr_GiB": round(p / 2**30, 1),
+                              "one_launch_us": round(t1 * 1e3, 1), "dispatch_1GiB_launches_us": round(ta * 1e3, 1)}),
+                  flush=True)
 
 
 if __name__ == "__main__":
