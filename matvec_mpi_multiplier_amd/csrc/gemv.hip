@@ -813,10 +813,10 @@ static int launch(int v, const double* A, int64_t lda, const double* x, double* 
     }
     int64_t max_rows = max_blocks * var.rows_per_block;
     // One row per wave (short rows): at most 1 GiB of A per launch. A longer launch of this
-    // form streams at one of two rates from process to process (config 5's 16 GiB: 2.36-2.38 ms
-    // or 2.50-2.53 ms, the slow one in most processes); 1 GiB launches run at 2.35-2.36 ms in the
-    // slow case, 2.39-2.40 (the extra launch boundaries) in the fast one, and the 2 GiB shard at
-    // 292 instead of 301-310 us (round 3, profiles/r03/sublaunch/).
+    // form streams at one of two rates depending on where the buffer landed (config 5's 16 GiB:
+    // 2.37-2.38 ms or 2.50-2.53 ms, the slow placement in most bench runs); 1 GiB launches run at
+    // 2.34-2.36 ms on either (2.39-2.40 on some boxes' fast buffers: the extra launch boundaries),
+    // and the 2 GiB shard at 292 instead of 301-310 us (round 3, profiles/r03/sublaunch/).
     if (v == kVecOneRow) {
         int64_t cap = (kOneRowLaunchBytes / (lda * (int64_t)sizeof(double))) / var.rows_per_block * var.rows_per_block;
         if (cap < var.rows_per_block) cap = var.rows_per_block;
