@@ -1,7 +1,7 @@
 """Placement probe (development tool): the same GEMV variants on many freshly allocated buffers of
 one shape in one process, to find buffers whose placement reads slower and which kernel orders
 are immune to it. `pieces<n>` = the dispatch's kernel as n launches over consecutive row ranges;
-`stream` = the read-only stream kernel over A's bytes.
+`stream` = the read-only stream kernel over A's bytes; `exact` = the dispatch's bit-exact kernel.
 
     python tools/probes/placement_probe.py [--shape 16384x16384] [--buffers 12]
         [--variants auto,rowblk_w4_r2_u8_xcd,pieces2,stream]
@@ -59,7 +59,9 @@ def main():
             a = A.data_ptr()
             out = {"round": rnd, "buffer": b, "addr_GiB": round(a / 2**30, 2)}
             for name in args.variants.split(","):
-                if name == "stream":
+                if name == "exact":
+                    fn = (lambda: lib.mvg_gemv_exact(a, K, xp, yp, M, K, s))
+                elif name == "stream":
                     fn = (lambda: lib.mvg_stream_read(a, M * K, sink.data_ptr(), s))
                 elif name.startswith("pieces"):
                     n = int(name[6:])
