@@ -790,6 +790,7 @@ static int64_t split_count(const Variant& var, int64_t M, int64_t K, bool force)
 // HIP caps a launch at gridDim.x * blockDim.x < 2^32 threads: very tall problems run as
 // several launches over consecutive row ranges (each range is an independent GEMV).
 constexpr int64_t kOneRowLaunchBytes = 1ll << 30;
+constexpr int64_t kMinPieceRows = 65536;
 static int launch(int v, const double* A, int64_t lda, const double* x, double* y, int64_t M,
                   int64_t K, hipStream_t s, bool force_split) {
     const Variant& var = kVariants[v];
@@ -817,9 +818,12 @@ static int launch(int v, const double* A, int64_t lda, const double* x, double* 
     // 2.37-2.38 ms or 2.50-2.53 ms, the slow placement in most bench runs); 1 GiB launches run at
     // 2.34-2.36 ms on either (2.39-2.40 on some boxes' fast buffers: the extra launch boundaries),
     // and the 2 GiB shard at 292 instead of 301-310 us (round 3, profiles/r03/sublaunch/).
+    // (1 GiB of the bytes read, k per row — a view's wider lda does not shrink the pieces — and
+    // never under 65536 rows, so a launch still fills the chip)
     if (v == kVecOneRow) {
-        int64_t cap = (kOneRowLaunchBytes / (lda * (int64_t)sizeof(double))) / var.rows_per_block * var.rows_per_block;
-        if (cap < var.rows_per_block) cap = var.rows_per_block;
+        int64_t cap = kOneRowLaunchBytes / (K * (int64_t)sizeof(double));
+        if (cap < kMinPieceRows) cap = kMinPieceRows;
+        cap = cap / var.rows_per_block * var.rows_per_block;
         if (cap < max_rows) max_rows = cap;
     }
     for (int64_t r0 = 0; r0 < M; r0 += max_rows) {

@@ -789,6 +789,7 @@ constexpr int64_t kPanelWidth = 256;
 
 constexpr int64_t kShortRowK = 768;
 constexpr int64_t kShortRowLaunchBytes = 1ll << 30;
+constexpr int64_t kMinPieceRows = 65536;
 
 // one form for every shape: 24 segments in flight gained only 1-2 % from 32768 rows (round 2),
 // inside the box-to-box spread, so round 3 dropped that threshold
@@ -838,9 +839,12 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
     // short rows (K <= 768): at most 1 GiB of A per launch, as the tree form's one-row waves
     // (gemv.hip): config 5's 16 GiB in 2.46 ms instead of 2.58, its 2 GiB shard 316 against
     // 318 us (round 3, profiles/r03/sublaunch/)
-    if (k > 0 && k <= kShortRowK) {  // (k > 0: then lda >= k >= 1)
-        int64_t cap = kShortRowLaunchBytes / (lda * (int64_t)sizeof(double)) / var.rows * var.rows;
-        if (cap < var.rows) cap = var.rows;
+    // (1 GiB of the bytes read, k per row, never under 65536 rows: a view's wider lda does not
+    // shrink the pieces below what fills the chip)
+    if (k > 0 && k <= kShortRowK) {
+        int64_t cap = kShortRowLaunchBytes / (k * (int64_t)sizeof(double));
+        if (cap < kMinPieceRows) cap = kMinPieceRows;
+        cap = cap / var.rows * var.rows;
         if (cap < max_rows) max_rows = cap;
     }
     const size_t lds = var.xlds ? (size_t)k * sizeof(double) : 0;

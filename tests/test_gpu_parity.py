@@ -101,35 +101,38 @@ def test_gemv_rejects_bad_arguments():
             mm.gemv(*args)
 
 
-def test_one_row_form_runs_in_1_gib_launches_with_ragged_tail():
-    # short rows (one row per wave) with more than 1 GiB of A go out as launches of <= 1 GiB
-    # (gemv.hip kOneRowLaunchBytes): rows on both sides of each piece boundary and the ragged
-    # last piece must match the oracle, and the auto path must equal the explicit variant
+@pytest.mark.parametrize("lda_mult", [1, 2])
+def test_one_row_form_runs_in_1_gib_launches_with_ragged_tail(lda_mult):
+    # short rows (one row per wave) reading more than 1 GiB go out as launches of <= 1 GiB of
+    # the bytes read (gemv.hip kOneRowLaunchBytes; a view's wider lda does not shrink them): rows
+    # on both sides of each piece boundary and the ragged last piece must match the oracle, and
+    # the auto path must equal the explicit variant
     k = 300
-    piece = (1 << 30) // (8 * k) // 4 * 4  # rows per launch: 1 GiB of A, whole 4-row workgroups
+    lda = k * lda_mult
+    piece = (1 << 30) // (8 * k) // 4 * 4  # rows per launch: 1 GiB read, whole 4-row workgroups
     m = 2 * piece + 37
-    v = _lib.lib.mvg_gemv_auto_variant(k, m, k)
+    v = _lib.lib.mvg_gemv_auto_variant(lda, m, k)
     assert _lib.lib.mvg_gemv_variant_name(v).decode() == "vec_l64_r1_u4_nt1_o5"
-    dA, dx, dy = mm.DeviceBuffer(m * k), mm.DeviceBuffer(k), mm.DeviceBuffer(m)
-    _lib.check(_lib.lib.mvg_synth_fill_device(dA.ptr, k, m, k, 0, 0, k, 42, None), "fill A")
+    dA, dx, dy = mm.DeviceBuffer(m * lda), mm.DeviceBuffer(k), mm.DeviceBuffer(m)
+    _lib.check(_lib.lib.mvg_synth_fill_device(dA.ptr, lda, m, lda, 0, 0, lda, 42, None), "fill A")
     x = oracle.synth(1, k, 4242)[0]
     dx.upload(x)
-    mm.gemv(dA.ptr, k, dx.ptr, dy.ptr, m, k)
+    mm.gemv(dA.ptr, lda, dx.ptr, dy.ptr, m, k)
     _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
     y = dy.download()
-    for r0 in (0, piece - 3, 2 * piece - 3, m - 40):
-        want = oracle.multiply_std_rowwise(oracle.synth_block(r0, 40, 0, k, k, 42), x)
+    rows = (0, piece - 3, 2 * piece - 3, m - 40)
+    wants = [oracle.multiply_std_rowwise(oracle.synth_block(r0, 40, 0, k, lda, 42), x) for r0 in rows]
+    for r0, want in zip(rows, wants):
         assert max_rel(y[r0:r0 + 40], want) <= TOL, r0
     assert y.min() >= 0 and y.max() <= k * 0.9999 * 0.9999
-    mm.gemv(dA.ptr, k, dx.ptr, dy.ptr, m, k, None, v)
+    mm.gemv(dA.ptr, lda, dx.ptr, dy.ptr, m, k, None, v)
     _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
     np.testing.assert_array_equal(dy.download(), y)
     # the exact kernels split short rows the same way (gemv_exact.hip kShortRowLaunchBytes)
-    _lib.check(_lib.lib.mvg_gemv_exact(dA.ptr, k, dx.ptr, dy.ptr, m, k, None), "exact")
+    _lib.check(_lib.lib.mvg_gemv_exact(dA.ptr, lda, dx.ptr, dy.ptr, m, k, None), "exact")
     _lib.check(_lib.lib.mvg_stream_sync(None), "sync")
     ye = dy.download()
-    for r0 in (0, piece - 3, 2 * piece - 3, m - 40):
-        want = oracle.multiply_std_rowwise(oracle.synth_block(r0, 40, 0, k, k, 42), x)
+    for r0, want in zip(rows, wants):
         np.testing.assert_array_equal(ye[r0:r0 + 40], want, err_msg=str(r0))
 
 
