@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--ref-rows", type=int, default=1024,
                     help="rows of the sample the real reference runs on (its loop is 100 iterations)")
     ap.add_argument("--ref-timeout", type=float, default=240.0)
+    ap.add_argument("--cpu-sweep", default="1,2,4,8",
+                    help="rank counts the real reference also runs at on the headline sample (cpu_baseline.sweep), "
+                         "besides the host's CPU quota; '' skips the sweep")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs 3-5 section")
     ap.add_argument("--configs", default="3,4,5", help="which BASELINE configs the section runs, in order")
     ap.add_argument("--config-steps", type=int, default=20)
@@ -90,21 +93,94 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(alg: str, R: int, C: int, n: int):
-    """HBM bytes per GEMV launch from the committed rocprofv3 PMC summary for this config
-    (profiles/*pmc*.json written by tools/pmc_traffic.py), or None."""
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
+FAILURES: list[str] = []  # the bench's parity checks that failed (JSON `failures`; exit code 1)
+
+
+def expect(cond, msg) -> bool:
+    """One of the bench's correctness checks (y against the oracle, the reference's own rows, the
+    tree form, ...). A failure is logged and kept for the JSON line's `failures` and the run goes
+    on to its end (at N > 1 every rank must still reach the same collectives), then exits 1."""
+    if not cond:
+        log(f"bench: CHECK FAILED: {msg}")
+        FAILURES.append(str(msg)[:300])
+    return bool(cond)
+
+
+def kernel_family(variant: str) -> str:
+    """The kernel template a dispatch variant name instantiates (the PMC summaries' key)."""
+    for prefix, fam in (("rowlines", "gemv_rowblock_lines"), ("rowblk", "gemv_rowblock"), ("vec", "gemv_vec"),
+                        ("scl", "gemv_scalar"), ("hopxl", "gemv_seq_hop_xl"), ("hop", "gemv_seq_hop"),
+                        ("seqx", "gemv_seq_x"), ("seq_", "gemv_seq"), ("panel", "gemv_seq_hop_panel")):
+        if variant.startswith(prefix):
+            return fam + ("_split" if variant.endswith("_splitk") else "")
+    return variant
+
+
+def pmc_summary(M: int, K: int, variant: str):
+    """The newest committed rocprofv3 PMC summary (tools/pmc_traffic.py ->
+    profiles/<round>/pmc_<family>_<M>x<K>.json) for this kernel family on an M x K shard: HBM bytes
+    per launch (`traffic`), VALU busy, L2 hit rate, memory-side read latency and reads in flight,
+    or None when no summary matches."""
+    fam = kernel_family(variant)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("alg") == alg and d.get("R") == R // n and d.get("C") == C:
-            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
-    return None, None
+        if d.get("kernel_family") == fam and d.get("M") == M and d.get("K") == K:
+            out = {k: (round(d[k], 4) if isinstance(d[k], float) else d[k]) for k in (
+                "hbm_bytes_per_launch", "traffic_over_algorithmic", "valu_busy", "l2_hit", "ea_read_latency_cyc",
+                "ea_reads_in_flight", "dram_read_frac") if d.get(k) is not None}
+            out["source"] = os.path.relpath(path, REPO)
+            return out
+    return None
+
+
+def launcher_cmd(argv: list[str], n: int, port: int) -> list[str]:
+    """The driver's N-GPU command for this same invocation: torch.distributed.run with one rank
+    per GPU on this node, rendezvous on 127.0.0.1 (the container hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def relay(cmd: list[str], env: dict | None = None) -> int:
+    """Run `cmd` as a child process (never exec: the parent has not touched the GPU, and must not
+    be replaced after it has), pass its stderr through, print the one JSON line its rank 0 wrote
+    on stdout (every other stdout line goes to stderr), and return its exit code (1 if it exited
+    0 without a JSON line)."""
+    import subprocess
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for ln in p.stdout:
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        elif s:
+            print(s, file=sys.stderr, flush=True)
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        log("bench: the ranks exited without a JSON line")
+        return 1
+    return rc
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` with no launcher: start the N ranks ourselves (the reference's
+        # own sweep is `mpiexec -n $np`, test.sh:5-11) and relay rank 0's line and the exit code
+        sys.exit(relay(launcher_cmd(sys.argv[1:], args.gpus, free_port())))
     # stdout carries exactly one JSON line (rank 0): anything the runtimes print on fd 1
     # (RCCL's init banner, HIP messages) is sent to stderr instead.
     json_out = os.fdopen(os.dup(1), "w")
@@ -113,12 +189,12 @@ def main():
     # one process per GPU: CUDA-tensor / RCCL IPC between processes needs the dmabuf IPC mode on
     # this ROCm (the legacy handle path fails with hipIpcGetMemHandle: invalid argument); set before
     # the HIP runtime starts. With N > 1, RCCL logs its transport choices to a per-rank file that
-    # rccl_report() reads back (P2P/IPC over xGMI, or SHM / NET), unless the caller set NCCL_DEBUG.
+    # rccl_report() reads back (P2P/IPC over xGMI, or SHM / NET), unless the caller set NCCL_DEBUG
+    # or NCCL_DEBUG_FILE: then RCCL logs as the caller asked and the report is skipped.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    # (INFO goes to the file only, so a caller's quieter NCCL_DEBUG level on stderr is unaffected;
-    # a caller who directs RCCL's log to a file of their own keeps it, and the report is skipped)
     rccl_log, caller_debug = None, os.environ.get("NCCL_DEBUG")
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG_FILE" not in os.environ:
+    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and caller_debug is None
+            and "NCCL_DEBUG_FILE" not in os.environ):
         rccl_log = f"/tmp/mvg_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log"
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=rccl_log)
     import torch
@@ -197,12 +273,13 @@ def main():
     # (N = 1) and by tests/.
     y = eng.collect()
     if rank == 0:
-        assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, "y out of range"
+        expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, "y out of range")
 
     # ---- the same workload in bit-exact mode (the reference's sequential sums, bit for bit)
-    # The sections after the headline are reported beside it; in one process (no other rank
-    # waiting in a collective) a failing section is recorded in its place instead of taking the
-    # headline line down with it. With N > 1 ranks a failure still ends the run, as it must.
+    # The sections after the headline are reported beside it. Their parity checks never raise
+    # (expect(): recorded, exit code 1 at the end). Any other error — the environment's: out of
+    # memory, a missing reference binary — is recorded in the section's place in one process (no
+    # other rank waiting in a collective) and ends the run with N > 1 ranks, as it must.
     def guarded(fn, *a):
         if distributed:
             return fn(*a)
@@ -245,7 +322,8 @@ def main():
     # ---- CPU baseline: rank 0 at N = 1 only
     cpu = None
     if rank == 0 and n == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.alg, R, C, y, y_exact)
+        cpu = cpu_baseline(args, args.alg, R, C, y, y_exact,
+                           sweep_ps=tuple(int(p) for p in args.cpu_sweep.split(",") if p.strip()))
         same_port, same_ref = cpu.pop("exact_vs_port", None), cpu.pop("exact_vs_reference", None)
         if exact is not None:
             # rowwise: the exact y against the oracle port's y (full matrix) and against the real
@@ -263,7 +341,7 @@ def main():
         ref_rows = reference_rows_check("config 2", "rowwise", R, C, n, y, y_exact)
 
     if rank == 0:
-        traffic, traffic_src = pmc_traffic(args.alg, R, C, n)
+        pmc = pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)) or {}
         out = {
             "metric": "fp64 GEMV achieved HBM GB/s per GPU + end-to-end time at 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -293,12 +371,14 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                "traffic": traffic,
+                "traffic": pmc.get("hbm_bytes_per_launch"),
+                "valu_busy": pmc.get("valu_busy"),
+                "l2_hit": pmc.get("l2_hit"),
                 "kernel": kernel_name(sh) + ", per GPU",
                 "kernel_ms": round(kernel_ms, 5),
                 "kernel_ms_by_rank": kernel_by_rank,
                 "bytes_per_launch": per_gpu,
-                "traffic_source": traffic_src,
+                "pmc": pmc or None,
             },
             "cpu_baseline": cpu,
             "reference_rows": ref_rows,
@@ -308,14 +388,84 @@ def main():
             "loader": loader,
             "end_to_end": e2e,
             "configs": configs,
+            "single_process": None,
         }
-        json_out.write(json.dumps(out) + "\n")
-        json_out.flush()
 
     eng.destroy()
     comm.destroy()
     if distributed:
         dist.destroy_process_group()
+    if rank == 0:
+        if n > 1:
+            # the executables' one-process-drives-N-GPUs path (ncclCommInitAll, grouped exchange),
+            # which the rank-per-GPU sections above never run; the other ranks have exited
+            out["single_process"] = single_process_section(args, n, R, C, rccl_log is not None)
+        out["failures"] = FAILURES or None
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
+    if FAILURES:
+        sys.exit(1)
+
+
+def single_process_section(args, n, R, C, we_set_nccl_debug):
+    """The drop-in executables' single-process form of the same workload: ONE process drives all
+    N GPUs (mvg_comm_init_all -> ncclCommInitAll over N devices, the grouped ncclCommSplit and the
+    exchange grouped over the local devices, csrc/engine.cpp), which the one-rank-per-GPU
+    sections above never run. Rank 0 starts `MVG_NGPUS=N MVG_SYNTH=device bin/multiplier_<alg>
+    R C` as a child process once the process group is gone, and records its device-resident line
+    and its y against config 2's reference rows. A failure is recorded here, never fatal; the
+    reference's own grid and gather: multiplier_blockwise.c:299-306, :144-210."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+
+    import torch
+
+    have = torch.cuda.device_count()
+    if have < n or os.environ.get("MVG_SAME_DEVICE") == "1":
+        return {"ran": False, "why": f"needs {n} devices in one process, {have} visible"
+                + (" (MVG_SAME_DEVICE rehearsal: every rank on one GPU)" if os.environ.get("MVG_SAME_DEVICE") == "1" else "")}
+    exe = os.path.join(REPO, "bin", f"multiplier_{args.alg}")
+    if not os.access(exe, os.X_OK):
+        return {"ran": False, "why": f"{os.path.relpath(exe, REPO)} not built"}
+    work = tempfile.mkdtemp(prefix="mvg_single_")
+    try:
+        ypath = os.path.join(work, "y.txt")
+        drop = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT"}
+        if we_set_nccl_debug:
+            drop |= {"NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE"}
+        env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC")}
+        iters = 50
+        env.update(MVG_NGPUS=str(n), MVG_SYNTH="device", MVG_ITERS=str(iters), MVG_Y_OUT=ypath)
+        cmd = [exe, str(R), str(C)]
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=300)
+        wall = time.perf_counter() - t0
+        out = {"ran": True, "command": f"MVG_NGPUS={n} MVG_SYNTH=device MVG_ITERS={iters} "
+                                      f"bin/multiplier_{args.alg} {R} {C}", "rc": r.returncode,
+               "wall_s": round(wall, 2)}
+        m = re.search(r"device-resident: ([\d.]+) ms per multiply, ([\d.]+) GB/s aggregate; GEMV kernel ([\d.]+) ms",
+                      r.stdout)
+        if r.returncode != 0 or not m or not os.path.exists(ypath):
+            out["error"] = (r.stdout[-300:] + " | " + r.stderr[-500:]).strip()
+            expect(False, f"single-process executable failed (rc {r.returncode})")
+            return out
+        out.update(ms_per_step=float(m.group(1)), value=float(m.group(2)), unit="GB/s",
+                   kernel_ms=float(m.group(3)))
+        m2 = re.search(r"end-to-end \(([^)]*)\): mean ([\d.]+) s", r.stdout)
+        if m2:
+            out["end_to_end_s"] = float(m2.group(2))
+        y = np.loadtxt(ypath, dtype=np.float64, ndmin=1)
+        expect(y.shape == (R,), f"single-process y has {y.shape} elements, want {R}")
+        if args.alg == "rowwise" and C == SHARD and R >= SHARD and y.shape == (R,):
+            out["reference_rows"] = reference_rows_check("config 2", args.alg, R, C, n, y, None)
+        return out
+    except Exception as exc:  # recorded, never fatal: the rank sections' line still prints
+        return {"ran": False, "error": f"{type(exc).__name__}: {str(exc)[:300]}"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
 
 
 def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, total_bytes, y_tree):
@@ -379,12 +529,14 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
            "kernel": kernel,
            "kernel_ms": round(kms, 5),
            "roofline_frac": frac(kms),
+           "pmc": pmc_summary(eng.shard(0).n_rows, eng.shard(0).n_cols, kernel),
            "row_major": {"value": round(total_bytes * steps / rel_ / 1e9, 1), "ms_per_step": round(rel_ / steps * 1e3, 4),
-                         "kernel": rkernel, "kernel_ms": round(rkms, 5), "roofline_frac": frac(rkms)}}
+                         "kernel": rkernel, "kernel_ms": round(rkms, 5), "roofline_frac": frac(rkms),
+                         "pmc": pmc_summary(eng.shard(0).n_rows, eng.shard(0).n_cols, rkernel)}}
     if rank == 0:
         rel = float(np.max(np.abs(y - y_tree) / np.abs(y_tree)))
-        assert rel <= 1e-12, f"exact y differs from the tree-summed y by {rel}"
-        assert np.array_equal(y, y_rm), "the panel and row-major exact kernels differ"
+        expect(rel <= 1e-12, f"exact y differs from the tree-summed y by {rel}")
+        expect(np.array_equal(y, y_rm), "the panel and row-major exact kernels differ")
         out["max_rel_vs_tree"] = rel
     return out, y
 
@@ -437,7 +589,7 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
                 "speedup_vs_separate": round(nv * single / ms, 3),
                 "kernel": lib.mvg_gemv_multi_variant_name(lib.mvg_gemv_multi_auto_variant(K, K, M, K, nv)).decode(),
             }
-        assert worst <= 1e-12, f"multi-vector y differs from the single-vector y by {worst}"
+        expect(worst <= 1e-12, f"multi-vector y differs from the single-vector y by {worst}")
         out["max_rel_vs_single"] = worst
         return out
     finally:
@@ -484,7 +636,7 @@ def loader_section(R, C):
             el = time.perf_counter() - t0
             best = el if best is None else min(best, el)
         same = bool(np.array_equal(A, mm.synth_host(R, C, 42)))
-        assert same, "the loader's matrix differs from the synthetic values its file holds"
+        expect(same, "the loader's matrix differs from the synthetic values its file holds")
         del A
         return {"file": os.path.basename(path), "text_bytes": nbytes, "parse_s": round(best, 4),
                 "GBps_text": round(nbytes / best / 1e9, 2), "write_s": round(wrote, 3),
@@ -572,7 +724,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             y = e.collect()
             yx = None
             if rank == 0:
-                assert np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range"
+                expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range")
             if not args.no_exact:
                 # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
                 # every partial to rank 0, the reference's combine order there)
@@ -588,11 +740,11 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
                          "gflops": round(2 * R * C * xsteps / xel / 1e9, 1),
                          "steps": xsteps, "kernel": xkernel, "kernel_ms": round(xkms, 5),
-                         "kernel_ms_by_rank": by_rank[0],
+                         "kernel_ms_by_rank": by_rank[0], "pmc": pmc_summary(sh.n_rows, sh.n_cols, xkernel),
                          "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
                 if rank == 0:
                     rel = float(np.max(np.abs(yx - y) / np.abs(y)))
-                    assert rel <= 1e-12, f"{name}: exact y differs from the tree-summed y by {rel}"
+                    expect(rel <= 1e-12, f"{name}: exact y differs from the tree-summed y by {rel}")
                     exact["max_rel_vs_tree"] = rel
         finally:
             e.destroy()
@@ -605,6 +757,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             "gflops": round(2 * R * C * args.config_steps / el / 1e9, 1),
             "kernel": kernel_name(sh), "kernel_ms": round(kms, 5), "kernel_ms_by_rank": tree_by_rank,
             "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
+            "pmc": pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)),
             "exact": exact,
         }
         if rank == 0:
@@ -644,7 +797,7 @@ def reference_rows_check(name, alg, R, C, n, y, yx):
             return {"P": n, "checked": False, "why": f"no reference slice for P = {n}"}
         rows, want = z[f"{key_cfg}/rows"], z[key]
     rel = float(np.max(np.abs(y[rows] - want) / np.abs(want)))
-    assert rel <= 1e-12, f"{name}: y differs from the reference's own y on its rows by {rel}"
+    expect(rel <= 1e-12, f"{name}: y differs from the reference's own y on its rows by {rel}")
     out = {"P": n, "rows": int(len(rows)), "max_rel": rel,
            "source": "tests/golden/config_slices.npz: oracle/_ref, mpiexec -n P, on 4 bands of the config's rows"
                      + ("" if key.endswith(f"/P{n}") else f" (reference run at {key.split('/')[-1]}: row sums do not depend on P)")}
@@ -702,7 +855,8 @@ def rccl_report(path, distributed, rank):
     """What RCCL reported about its communicators, all ranks gathered on rank 0: the transport of
     every connection it set up ("a->b": P2P/IPC, P2P/direct pointer, SHM, NET/...), counted per
     transport, and the communicator sizes (nranks) it initialised. Parsed from the NCCL_DEBUG=INFO
-    file each rank wrote (NCCL_DEBUG_FILE); None when the caller set NCCL_DEBUG itself."""
+    file each rank wrote (NCCL_DEBUG_FILE); {"logged": false, ...} when the caller set NCCL_DEBUG
+    or NCCL_DEBUG_FILE (RCCL then logs where the caller asked, untouched)."""
     import torch.distributed as dist
 
     mine = {"links": {}, "nranks": [], "samples": []}
@@ -718,7 +872,7 @@ def rccl_report(path, distributed, rank):
     if rank != 0:
         return None
     if path is None:
-        return {"logged": False, "why": "NCCL_DEBUG_FILE set by the caller"}
+        return {"logged": False, "why": "NCCL_DEBUG or NCCL_DEBUG_FILE set by the caller"}
     links, counts, sizes, samples = {}, {}, set(), []
     for r in allr:
         sizes.update(r["nranks"])
@@ -758,7 +912,7 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             times.append(float(tt[0]))
         if rank == 0:
-            assert np.array_equal(y, y_ref), "end-to-end y differs from the device-resident y"
+            expect(np.array_equal(y, y_ref), "end-to-end y differs from the device-resident y")
         return {"mean_s": float(np.mean(times)), "iters": len(times),
                 "GBps": total_bytes / float(np.mean(times)) / 1e9,
                 "gflops": 2 * R * C / float(np.mean(times)) / 1e9}
@@ -858,12 +1012,14 @@ def pcie_roofline(local):
 
 
 def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_bytes=None, cpu_seconds=None,
-                 placements=("spread", "compact")):
+                 placements=("spread", "compact"), sweep_ps=()):
     """The reference's CPU path timed on this host. Preferred: the real reference (oracle/_ref,
     built from its own sources, run with MPICH's mpiexec on P = the port's thread count) on the
     leading `ref_rows` rows of the same matrix, kind "reference"; its 100-iteration loop is fixed
     in its source. Always also: the oracle port (below), reported under "port" (or as the
-    baseline itself, kind "port", when the reference cannot run here)."""
+    baseline itself, kind "port", when the reference cannot run here). `sweep_ps`: the reference
+    also runs on the same sample at those rank counts (`sweep`: its time, GB/s, speed-up and
+    efficiency as its README defines them, S = T1 / TP and E = S / P, README.md:47-50)."""
     ref_rows = args.ref_rows if ref_rows is None else ref_rows
     port = cpu_port_baseline(args, alg, R, C, y_gpu, y_exact, sample_bytes, cpu_seconds)
     if args.no_ref_baseline:
@@ -901,9 +1057,11 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
     label, cpus, r = min(runs, key=lambda t: t[2]["seconds"])
     placements = {lab: round(8 * (rows * C + C + rows) / rr["seconds"] / 1e9, 3) for lab, _, rr in runs}
     rel = float(np.max(np.abs(y_gpu[:rows] - r["y"]) / np.abs(r["y"])))
-    assert rel <= 1e-12, f"GPU y differs from the reference's own y: {rel}"
+    expect(rel <= 1e-12, f"GPU y differs from the reference's own y: {rel}")
     nbytes = 8 * (rows * C + C + rows)
+    sweep = ref_sweep(args, alg, rows, C, P, r["seconds"], label, sweep_ps, nbytes) if sweep_ps else None
     return {"value": round(nbytes / r["seconds"] / 1e9, 3), "unit": "GB/s", "cores": P, "kind": "reference",
+            "sweep": sweep,
             "ms_per_step": round(r["seconds"] * 1e3, 3), "iters": 100,
             "sample": f"leading {rows} of {R} rows ({rows}x{C}) {alg}: the reference's own executable "
                       f"(oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its text inputs, its "
@@ -914,6 +1072,33 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
             "exact_vs_port": port.get("exact_vs_port"),
             **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}
                if y_exact is not None and alg == "rowwise" else {})}
+
+
+def ref_sweep(args, alg, rows, C, P, seconds_at_P, label_at_P, ps, nbytes):
+    """The real reference on the same leading-rows sample at each rank count in `ps` (and at P,
+    already run): mpiexec -n p, confined to p CPUs of the GPU's NUMA node first (oracle/cpuset),
+    its own 100-iteration loop. The reference's scaling sweep is `mpiexec -n $np` over np in
+    {1, 2, 6, 12, 24} (test.sh:5-11); speed-up S = T1 / TP, efficiency E = S / P
+    (README.md:47-50). Rank counts that do not split the sample are skipped."""
+    from oracle import cpuset, ref_runner
+
+    times, where, errors = {P: seconds_at_P}, {P: label_at_P}, []
+    for p in sorted(set(ps)):
+        if p == P or p > P or p < 1 or not _splits(alg, rows, C, p):
+            continue
+        try:
+            rr = ref_runner.run(alg, rows, C, p, timeout=args.ref_timeout, cpus=cpuset.pick(p, gpu_numa_node()),
+                                rows=np.arange(rows))
+            times[p], where[p] = rr["seconds"], "spread"
+        except Exception as exc:  # a sweep point must never sink the bench
+            errors.append(f"P={p}: {str(exc)[:160]}")
+    t1 = times.get(1)
+    pts = [{"P": p, "s_per_iter": round(t, 6), "GBps": round(nbytes / t / 1e9, 3),
+            "speedup": round(t1 / t, 3) if t1 else None, "efficiency": round(t1 / t / p, 3) if t1 else None,
+            "placement": where[p]} for p, t in sorted(times.items())]
+    return {"points": pts, "errors": errors or None,
+            "semantics": "the reference's own executable on the sample above, mpiexec -n P; S = T1/TP, E = S/P "
+                         "(README.md:47-50)"}
 
 
 def cpu_port_baseline(args, alg, R, C, y_gpu, y_exact=None, sample_bytes=None, cpu_seconds=None):
@@ -952,14 +1137,14 @@ def cpu_port_baseline(args, alg, R, C, y_gpu, y_exact=None, sample_bytes=None, c
         t, y_cpu = oracle.time_multiply(alg, A, x, threads, iters)
     del A
     rel = float(np.max(np.abs(y_gpu[:rows] - y_cpu) / np.abs(y_cpu)))
-    assert rel <= 1e-12, f"GPU y differs from the reference restatement: {rel}"
+    expect(rel <= 1e-12, f"GPU y differs from the reference restatement: {rel}")
     exact_same = None
     if y_exact is not None and alg == "rowwise":
         # row sums do not depend on the rank count, so the port's P-rank y is the reference's y
         # for the GPU's single shard too; the exact mode must reproduce it bit for bit (the
         # column and block splits' combine orders depend on P, and the GPU runs P = N here)
         exact_same = bool(np.array_equal(y_exact[:rows], y_cpu))
-        assert exact_same, "exact-mode y differs from the reference restatement"
+        expect(exact_same, "exact-mode y differs from the reference restatement")
     nbytes = 8 * (rows * C + C + rows)
     what = "full workload" if rows == R else f"sample: leading {rows} of {R} rows"
     return {"exact_vs_port": exact_same, "value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": threads,

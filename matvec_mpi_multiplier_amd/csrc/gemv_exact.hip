@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A,
         // segments (config 5's 512 columns) needs no masked tail, whose loads would not be in
         // flight ahead of the chain
         nseg = lines_aligned(A, lda) ? K / S : K >= 15 ? (K - 15) / S : 0;
-        ntail = (K - nseg * S + S - 1) / S;            // the most any row has left: 1 or 2 segments
+        ntail = (K - nseg * S + S - 1) / S;            // what any row has left: 0, 1 or 2 segments (0: line-aligned rows of whole segments)
         const double* ar = arow + h;
         const double* xr = x + h;
         if (nseg > 0) {
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(64 * NW) void gemv_seq_hop_xl(const double* __restr
         const int64_t h = (int64_t)(((128u - ((uintptr_t)arow & 127u)) & 127u) >> 3);
         sum = hop_masked_segment<L, W>(sum, arow, x, h - S + off[0], 0, h < K ? h : K, true);
         nseg = lines_aligned(A, lda) ? K / S : K >= 15 ? (K - 15) / S : 0;
-        ntail = (K - nseg * S + S - 1) / S;
+        ntail = (K - nseg * S + S - 1) / S;  // 0, 1 or 2 tail segments, as in gemv_seq_hop
         const double* ar = arow + h;
         const double* xr = xl + h;
         auto xload = [&](const double* p, dbl2x (&d)[V]) {

@@ -1,6 +1,9 @@
-"""bench.py's host-side helpers on the CPU (no GPU): the RCCL transport report parser and the
-reference-row check every config's y goes through."""
+"""bench.py's host-side helpers on the CPU (no GPU): the RCCL transport report parser, the
+reference-row check every config's y goes through, the launcher relay that lets `bench.py --gpus N`
+run without torch.distributed.run, the check recorder and the PMC summary lookup."""
+import json
 import os
+import subprocess
 import sys
 
 import numpy as np
@@ -41,10 +44,12 @@ def test_reference_rows_check(cfg_name, alg, R, C, n):
     r = bench.reference_rows_check(cfg_name, alg, R, C, n, y, y.copy())
     assert r["P"] == n and r["rows"] == len(rows) and r["max_rel"] == 0.0 and r["exact_bit_identical"]
     assert ("exact_note" in r) == (alg == "blockwise" and n == 8)  # 2 x 4 grid: arrival-order sums
-    # a y off by more than the bar is refused, not reported
+    # a y off by more than the bar is a failed check: recorded (the run then exits 1), not raised
     y[rows[0]] *= 1 + 1e-10
-    with pytest.raises(AssertionError):
-        bench.reference_rows_check(cfg_name, alg, R, C, n, y, None)
+    bench.FAILURES.clear()
+    bench.reference_rows_check(cfg_name, alg, R, C, n, y, None)
+    assert len(bench.FAILURES) == 1 and "reference's own y" in bench.FAILURES[0]
+    bench.FAILURES.clear()
     # no reference slice at this P: recorded, not checked — except the row split, whose row sums
     # do not depend on P (its P = 1 slice stands for every P)
     r3 = bench.reference_rows_check(cfg_name, alg, R, C, 3, y, None) if alg != "rowwise" else None
@@ -60,3 +65,77 @@ def test_sample_splits_follow_the_reference_checks():
     assert bench._splits("rowwise", 128, 512, 16) and not bench._splits("rowwise", 100, 512, 16)
     assert bench._splits("colwise", 7, 65536, 16) and not bench._splits("colwise", 7, 100, 16)
     assert bench._splits("blockwise", 128, 131072, 16)  # 4 x 4 grid
+
+
+def test_expect_records_failures_and_returns_the_condition():
+    bench.FAILURES.clear()
+    assert bench.expect(True, "fine") is True and bench.FAILURES == []
+    assert bench.expect(False, "y differs") is False and bench.FAILURES == ["y differs"]
+    bench.FAILURES.clear()
+
+
+def test_launcher_cmd_is_the_drivers_n_gpu_command():
+    cmd = bench.launcher_cmd(["--gpus", "8", "--steps", "5"], 8, 29512)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29512" in cmd
+    assert cmd[-4:] == [os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "5"][-4:]
+    assert cmd[-5] == os.path.join(REPO, "bench.py")
+    assert 1024 <= bench.free_port() < 65536
+
+
+def _child(code):
+    return [sys.executable, "-c", code]
+
+
+def test_relay_prints_rank0_line_and_passes_the_exit_code(capsys):
+    line = json.dumps({"metric": "m", "value": 1.0})
+    rc = bench.relay(_child(f"print('RCCL banner'); print({line!r})"))
+    out = capsys.readouterr()
+    assert rc == 0 and out.out.strip() == line and "RCCL banner" in out.err
+    # a failing child: its exit code, even after a line
+    assert bench.relay(_child(f"import sys; print({line!r}); sys.exit(3)")) == 3
+    # exit 0 without a line is a failure too
+    assert bench.relay(_child("print('no json here')")) == 1
+
+
+def test_bench_without_launcher_starts_the_ranks_itself():
+    """`python bench.py --gpus 2` with no WORLD_SIZE: bench.py runs torch.distributed.run itself as
+    a child. Here (no GPU) the two ranks fail at their first GPU call, and that failure is the
+    command's exit code, with no JSON line on stdout."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
+    assert "torch.distributed" in r.stderr or "ChildFailedError" in r.stderr or "rank" in r.stderr.lower()
+
+
+def test_single_process_section_needs_n_devices():
+    class A:
+        alg = "rowwise"
+    r = bench.single_process_section(A(), 8, 8 * 16384, 16384, False)
+    assert r["ran"] is False and "needs 8 devices" in r["why"]
+
+
+def test_kernel_family_names():
+    assert bench.kernel_family("rowblk_w4_r2_u8") == "gemv_rowblock"
+    assert bench.kernel_family("rowblk_w8_r2_u4_splitk") == "gemv_rowblock_split"
+    assert bench.kernel_family("vec_l64_r1_u4_nt1_o5") == "gemv_vec"
+    assert bench.kernel_family("hop8_l8_w2_u16") == "gemv_seq_hop"
+    assert bench.kernel_family("hopxl_l8_w2_u16_n4") == "gemv_seq_hop_xl"
+    assert bench.kernel_family("seqx_r64_t16_b2_g8") == "gemv_seq_x"
+    assert bench.kernel_family("panel_l8_w2_u16 (column panels, P = 256)") == "gemv_seq_hop_panel"
+    assert bench.kernel_family("rowlines_w8_u4_x0") == "gemv_rowblock_lines"
+
+
+def test_pmc_summary_finds_the_committed_counters():
+    """The headline roofline's `traffic`, `valu_busy` and `l2_hit` come from the committed PMC
+    summaries (profiles/r04/pmc_<family>_<M>x<K>.json, tools/pmc_traffic.py)."""
+    d = bench.pmc_summary(16384, 16384, "rowblk_w4_r2_u8")
+    assert d is not None and d["source"].startswith("profiles/")
+    assert 0.99 < d["traffic_over_algorithmic"] < 1.01
+    assert 0.0 < d["valu_busy"] < 1.0 and 0.0 < d["l2_hit"] < 1.0
+    assert bench.pmc_summary(16384, 16384, "panel_l8_w2_u16 (column panels, P = 256)")["source"].endswith(
+        "pmc_gemv_seq_hop_panel_16384x16384.json")
+    assert bench.pmc_summary(3, 5, "rowblk_w4_r2_u8") is None

@@ -1,4 +1,4 @@
-"""The N > 1 path on CPU: world_size 2 and 4 over torch.distributed `gloo`.
+"""The N > 1 path on CPU: world_size 2, 4 and 8 over torch.distributed `gloo`.
 
 Each rank takes its shard from the C planner (mvg_plan_shard), computes its local product
 (with the oracle standing in for the GPU kernel — there is no GPU here), then runs the exchange

@@ -515,6 +515,40 @@ def test_device_numa_node_and_first_touch():
 
 # ---------------------------------------------------------------- chunked distribution overlap
 @pytest.mark.parametrize("alg", ["rowwise", "colwise", "blockwise"])
+def test_writes_right_after_a_chunked_distribution(comm1, alg):
+    """drain_chunks (csrc/engine.cpp): a chunked distribution's copies may still be running on the
+    copy stream when the next write of the shard is queued. A second distribute, or fill_synth,
+    with no multiply and no sync in between must land after them, and the next multiply must read
+    the whole new shard."""
+    R, C = 1000, 768
+    A1, A2 = oracle.synth(R, C, 42), oracle.synth(R, C, 7)
+    x1, x2 = oracle.synth(1, C, 4242)[0], oracle.synth(1, C, 99)[0]
+    for exact in (False, True):
+        with mm.Multiplier(alg, R, C, comm1, exact=exact) as e:
+            e.set_overlap(5)
+            ys = []
+            e.distribute(A1, x1)
+            e.distribute(A2, x2)  # chunked copies of A1 still queued: A2 must win
+            e.multiply()
+            ys.append(e.collect())
+            e.distribute(A2, x2)
+            e.fill_synth()  # seeds 42 / 4242: A1, x1 on the device, after A2's chunks
+            e.multiply()
+            ys.append(e.collect())
+            e.distribute(A2, x1)
+            e.set_overlap(0)
+            e.distribute(A1, x2)  # a whole-shard write while the chunks are still pending
+            e.multiply()
+            ys.append(e.collect())
+        for y, (A, x) in zip(ys, ((A2, x2), (A1, x1), (A1, x2))):
+            want = oracle.multiply(alg, A, x, 1)
+            if exact:
+                assert np.array_equal(y, want), alg
+            else:
+                assert max_rel(y, want) <= TOL, alg
+
+
+@pytest.mark.parametrize("alg", ["rowwise", "colwise", "blockwise"])
 @pytest.mark.parametrize("chunks", [2, 7])
 def test_overlapped_distribution_gives_the_same_y(comm1, alg, chunks):
     """mvg_engine_set_overlap: the shard goes over in row chunks and each chunk's GEMV runs behind

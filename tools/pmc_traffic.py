@@ -1,83 +1,126 @@
-"""Summarise rocprofv3 PMC passes for the GEMV kernel into profiles/<round>/pmc_<tag>.json.
+"""Summarise rocprofv3 PMC passes (tools/pmc_passes.sh) into one JSON per GEMV kernel family.
 
-    python tools/pmc_traffic.py --out profiles/r01/pmc_rowwise_16384.json --alg rowwise --R 16384 --C 16384 \
-        gpurun_out/pmc_fetch gpurun_out/pmc_write [gpurun_out/pmc_l2 ...]
+    python tools/pmc_traffic.py --outdir profiles/r04 --M 16384 --K 16384 [--pieces 1] \
+        gpurun_out/<run>/pmc/<variant>
 
-Each directory holds one `rocprofv3 --pmc ... --output-format csv` pass (counters collected in
-separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass). HBM bytes per launch follow
-MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports exactly
-half the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is
-exact for 16-B stores and uncalibrated for the GEMV's 8-B y stores (which are 8 B per row,
-negligible next to the A stream).
+Every directory below the given ones holds one `rocprofv3 --pmc ... --output-format csv` pass
+(counters collected in separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).
+Dispatches are grouped by kernel family (the template name: gemv_rowblock, gemv_vec,
+gemv_seq_hop, gemv_seq_hop_panel, ...), each family's counters reduced to the median over its
+dispatches, and written to OUTDIR/pmc_<family>_<M>x<K>.json. `--pieces n`: the library splits
+one call into n equal launches (config 5's short rows go out in 1 GiB launches), so one dispatch
+carries 1/n of the shape's algorithmic bytes.
+
+Derived fields (MI355X_MICROARCH.md §HBM and §rocprofv3; rocprofv3 sums a counter over its
+dimensions in the CSV, so GRBM_GUI_ACTIVE is the sum over the 8 XCDs):
+  hbm_bytes_per_launch  FETCH_SIZE x 1024 x 2 (gfx950 reports half of a wide stream) + WRITE_SIZE x 1024
+  valu_busy             SQ_ACTIVE_INST_VALU (quad-cycles, summed over SIMDs) / 256 CUs / (GRBM_GUI_ACTIVE / 8):
+                        the fraction of SIMD cycles issuing vector ALU work (rocprofv3's VALUBusy / 100)
+  l2_hit                TCC_HIT / (TCC_HIT + TCC_MISS)
+  ea_read_latency_cyc   TCC_EA0_RDREQ_LEVEL / TCC_EA0_RDREQ: mean cycles an L2 read miss is in flight
+  ea_reads_in_flight    TCC_EA0_RDREQ_LEVEL / (GRBM_GUI_ACTIVE / 8): mean memory-side reads in flight
+  dram_read_frac        TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ: reads the L2 sends to the HBM controllers.
+                        gfx950 exposes no Infinity-Cache (MALL) hit counter to rocprofv3 (no MALL_*
+                        block in `rocprofv3 -L`); its hits are inside these requests.
 """
 import argparse
 import csv
 import glob
 import json
 import os
+import re
 import statistics
 from collections import defaultdict
 
+CUS, XCDS = 256, 8
 
-def read_counters(d):
-    rows = []
-    for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
-        with open(path) as f:
-            rows += list(csv.DictReader(f))
-    per = defaultdict(dict)  # dispatch -> {counter: value}
+
+def family(kernel_name: str) -> str:
+    m = re.search(r"mvg::(\w+)", kernel_name)
+    return m.group(1) if m else kernel_name.split("(")[0]
+
+
+def read_dirs(dirs):
+    """{family: {counter: [value per dispatch]}} and the full template name seen per family."""
+    vals = defaultdict(lambda: defaultdict(list))
     names = {}
-    for r in rows:
-        kname = r.get("Kernel_Name", "")
-        disp = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        cname = r.get("Counter_Name")
-        val = float(r.get("Counter_Value", "nan"))
-        per[disp][cname] = per[disp].get(cname, 0.0) + val
-        names[disp] = kname
-    return per, names
+    for d in dirs:
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            per = defaultdict(dict)
+            kn = {}
+            with open(path) as f:
+                for r in csv.DictReader(f):
+                    disp = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                    c = r["Counter_Name"]
+                    per[disp][c] = per[disp].get(c, 0.0) + float(r["Counter_Value"])
+                    kn[disp] = r.get("Kernel_Name", "")
+            for disp, cs in per.items():
+                fam = family(kn[disp])
+                if not fam.startswith("gemv"):
+                    continue  # the synthetic fill, the panel relayout
+                names[fam] = kn[disp].split("(")[0].replace("void ", "")
+                for c, v in cs.items():
+                    vals[fam][c].append(v)
+    return vals, names
+
+
+def derive(med: dict, algo: int) -> dict:
+    out = {}
+    grbm = med.get("GRBM_GUI_ACTIVE")
+    if "FETCH_SIZE" in med:
+        fetch = 2.0 * med["FETCH_SIZE"] * 1024.0
+        write = med.get("WRITE_SIZE", 0.0) * 1024.0
+        out.update(hbm_read_bytes_per_launch=fetch, hbm_write_bytes_per_launch=write,
+                   hbm_bytes_per_launch=int(fetch + write), traffic_over_algorithmic=(fetch + write) / algo,
+                   correction="FETCH_SIZE x 1024 x 2 (gfx950 wide-stream half count) + WRITE_SIZE x 1024")
+    if "SQ_ACTIVE_INST_VALU" in med and grbm:
+        out["valu_busy"] = med["SQ_ACTIVE_INST_VALU"] / CUS / (grbm / XCDS)
+    if "SQ_INSTS_VALU" in med and "SQ_WAVES" in med and med["SQ_WAVES"]:
+        out["valu_insts_per_wave"] = med["SQ_INSTS_VALU"] / med["SQ_WAVES"]
+    if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
+        tot = med["TCC_HIT_sum"] + med["TCC_MISS_sum"]
+        out["l2_hit"] = med["TCC_HIT_sum"] / tot if tot else None
+    rd = med.get("TCC_EA0_RDREQ_sum")
+    if rd:
+        if "TCC_EA0_RDREQ_LEVEL_sum" in med:
+            out["ea_read_latency_cyc"] = med["TCC_EA0_RDREQ_LEVEL_sum"] / rd
+            if grbm:
+                out["ea_reads_in_flight"] = med["TCC_EA0_RDREQ_LEVEL_sum"] / (grbm / XCDS)
+        if "TCC_EA0_RDREQ_DRAM_sum" in med:
+            out["dram_read_frac"] = med["TCC_EA0_RDREQ_DRAM_sum"] / rd
+    if "TCP_UTCL1_REQUEST_sum" in med and med["TCP_UTCL1_REQUEST_sum"]:
+        out["utcl1_miss_rate"] = med.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0) / med["TCP_UTCL1_REQUEST_sum"]
+    if grbm:
+        out["grbm_cycles_per_xcd"] = grbm / XCDS
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
-    ap.add_argument("--out", required=True)
-    ap.add_argument("--alg", required=True)
-    ap.add_argument("--R", type=int, required=True)
-    ap.add_argument("--C", type=int, required=True)
-    ap.add_argument("--kernel", default="mvg::gemv_")
-    ap.add_argument("--bytes-per-launch", type=int, default=None)
+    ap.add_argument("--outdir", required=True)
+    ap.add_argument("--M", type=int, required=True, help="rows of the shape the probe multiplied")
+    ap.add_argument("--K", type=int, required=True)
+    ap.add_argument("--pieces", type=int, default=1, help="equal launches the library splits one call into")
+    ap.add_argument("--only", default=None, help="comma-separated kernel families to write")
     args = ap.parse_args()
-    counters = defaultdict(list)
-    for d in args.dirs:
-        per, names = read_counters(d)
-        for disp, cs in per.items():
-            if args.kernel in names[disp]:
-                for c, v in cs.items():
-                    counters[c].append(v)
-    med = {c: statistics.median(v) for c, v in counters.items()}
-    algo = args.bytes_per_launch or 8 * (args.R * args.C + args.C + args.R)
-    out = {"alg": args.alg, "R": args.R, "C": args.C, "kernel": args.kernel,
-           "launches": {c: len(v) for c, v in counters.items()}, "median_counters": med,
-           "algorithmic_bytes_per_launch": algo}
-    if "FETCH_SIZE" in med:
-        fetch = 2.0 * med["FETCH_SIZE"] * 1024.0  # gfx950: FETCH_SIZE = half of a wide stream
-        write = med.get("WRITE_SIZE", 0.0) * 1024.0
-        out["hbm_read_bytes_per_launch"] = fetch
-        out["hbm_write_bytes_per_launch"] = write
-        out["hbm_bytes_per_launch"] = int(fetch + write)
-        out["traffic_over_algorithmic"] = (fetch + write) / algo
-        out["correction"] = "FETCH_SIZE x 1024 x 2 (gfx950 wide-stream half count) + WRITE_SIZE x 1024"
-    for derived in ("VALUBusy", "VALUUtilization", "MemUnitStalled", "TA_BUSY_avr"):
-        if derived in med:
-            out[derived] = med[derived]
-    if "GRBM_GUI_ACTIVE" in med:
-        out["note_clock"] = "effective clock ~ GRBM_GUI_ACTIVE / 8 / kernel time (MI355X_MICROARCH.md)"
-    if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
-        tot = med["TCC_HIT_sum"] + med["TCC_MISS_sum"]
-        out["l2_hit_rate"] = med["TCC_HIT_sum"] / tot if tot else None
-    os.makedirs(os.path.dirname(args.out), exist_ok=True)
-    with open(args.out, "w") as f:
-        json.dump(out, f, indent=1)
-    print(json.dumps(out))
+    vals, names = read_dirs(args.dirs)
+    algo = 8 * (args.M * args.K + args.K + args.M) // args.pieces
+    os.makedirs(args.outdir, exist_ok=True)
+    for fam, cs in sorted(vals.items()):
+        if args.only and fam not in args.only.split(","):
+            continue
+        med = {c: statistics.median(v) for c, v in cs.items()}
+        out = {"kernel_family": fam, "kernel": names[fam], "M": args.M, "K": args.K, "pieces": args.pieces,
+               "dispatches": {c: len(v) for c, v in cs.items()}, "median_counters": med,
+               "algorithmic_bytes_per_launch": algo, **derive(med, algo),
+               "sources": [os.path.relpath(d) for d in args.dirs]}
+        path = os.path.join(args.outdir, f"pmc_{fam}_{args.M}x{args.K}.json")
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        print(path, json.dumps({k: out[k] for k in out if k in (
+            "traffic_over_algorithmic", "valu_busy", "l2_hit", "ea_read_latency_cyc", "ea_reads_in_flight",
+            "dram_read_frac", "utcl1_miss_rate")}))
 
 
 if __name__ == "__main__":
