@@ -188,13 +188,14 @@ def main():
     os.dup2(2, 1)
     # one process per GPU: CUDA-tensor / RCCL IPC between processes needs the dmabuf IPC mode on
     # this ROCm (the legacy handle path fails with hipIpcGetMemHandle: invalid argument); set before
-    # the HIP runtime starts. With N > 1, RCCL logs its transport choices to a per-rank file that
-    # rccl_report() reads back (P2P/IPC over xGMI, or SHM / NET), unless the caller set NCCL_DEBUG
-    # or NCCL_DEBUG_FILE: then RCCL logs as the caller asked and the report is skipped.
+    # the HIP runtime starts. With N > 1, RCCL logs at INFO to a per-rank file that rccl_report()
+    # reads back (the transport of every connection: P2P/IPC over xGMI, or SHM / NET); the WARN and
+    # ERROR lines of that file are passed on to stderr, so a caller's NCCL_DEBUG=WARN (or any
+    # level up to INFO; the pool's boxes export VERSION) loses nothing. A caller who sends RCCL's
+    # log to a file of their own (NCCL_DEBUG_FILE) keeps it untouched, and the report is skipped.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     rccl_log, caller_debug = None, os.environ.get("NCCL_DEBUG")
-    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and caller_debug is None
-            and "NCCL_DEBUG_FILE" not in os.environ):
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG_FILE" not in os.environ:
         rccl_log = f"/tmp/mvg_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log"
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=rccl_log)
     import torch
@@ -837,6 +838,11 @@ def parse_rccl_log(lines):
     return {"links": {k: sorted(v) for k, v in links.items()}, "nranks": nranks, "samples": samples}
 
 
+def rccl_warnings(lines):
+    """The WARN / ERROR lines of an RCCL log ("host:pid:tid [dev] NCCL WARN ...")."""
+    return [ln.rstrip() for ln in lines if " NCCL WARN " in ln or " NCCL ERROR " in ln]
+
+
 def per_rank(ms, distributed, local):
     """Every rank's mean GEMV time (ms), in rank order (None at N = 1): the max over ranks is the
     step's kernel time, the spread shows whether one GPU lags the others."""
@@ -855,14 +861,17 @@ def rccl_report(path, distributed, rank):
     """What RCCL reported about its communicators, all ranks gathered on rank 0: the transport of
     every connection it set up ("a->b": P2P/IPC, P2P/direct pointer, SHM, NET/...), counted per
     transport, and the communicator sizes (nranks) it initialised. Parsed from the NCCL_DEBUG=INFO
-    file each rank wrote (NCCL_DEBUG_FILE); {"logged": false, ...} when the caller set NCCL_DEBUG
-    or NCCL_DEBUG_FILE (RCCL then logs where the caller asked, untouched)."""
+    file each rank wrote (its WARN / ERROR lines go on to stderr); {"logged": false, ...} when the
+    caller set NCCL_DEBUG_FILE (RCCL then logs where the caller asked, untouched)."""
     import torch.distributed as dist
 
     mine = {"links": {}, "nranks": [], "samples": []}
     if path and os.path.exists(path):
         with open(path, errors="replace") as f:
-            mine = parse_rccl_log(f)
+            lines = f.readlines()
+        mine = parse_rccl_log(lines)
+        for line in rccl_warnings(lines):  # what a caller's NCCL_DEBUG=WARN would have shown
+            log(line)
         try:
             os.remove(path)
         except OSError:
@@ -872,7 +881,7 @@ def rccl_report(path, distributed, rank):
     if rank != 0:
         return None
     if path is None:
-        return {"logged": False, "why": "NCCL_DEBUG or NCCL_DEBUG_FILE set by the caller"}
+        return {"logged": False, "why": "NCCL_DEBUG_FILE set by the caller"}
     links, counts, sizes, samples = {}, {}, set(), []
     for r in allr:
         sizes.update(r["nranks"])

@@ -30,6 +30,9 @@ def test_parse_rccl_log_transports_and_sizes():
     assert r["nranks"] == [8, 4]
     assert len(r["samples"]) == 2 and "via P2P/IPC" in r["samples"][0]
     assert bench.parse_rccl_log([]) == {"links": {}, "nranks": [], "samples": []}
+    # the WARN / ERROR lines are passed on to stderr (a caller's NCCL_DEBUG=WARN loses nothing)
+    warn = "host:1234:1240 [0] NCCL WARN NET/Socket : message truncated"
+    assert bench.rccl_warnings(lines + [warn + "\n"]) == [warn]
 
 
 @pytest.mark.parametrize("cfg_name,alg,R,C,n", [("config 3", "colwise", 65536, 65536, 8),
