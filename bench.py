@@ -408,6 +408,32 @@ def main():
         sys.exit(1)
 
 
+def warm(e, min_launches, distributed, local, seconds=0.1):
+    """Untimed multiplies before a supplementary timed section: at least `min_launches`, and about
+    `seconds` of them, so that the section is timed at the clock a sustained run holds. The host
+    work between sections (y checks, D2H copies) idles the GPU long enough for it to drop its
+    clock, and the first milliseconds after that run slow; the memory-bound tree kernel does not
+    notice, the exact kernels (chain-paced, VALU busy 0.37-0.44) do (round 4: the row-major exact
+    form's first launches of a section 326-364 us against 313 us held). Every rank runs the same
+    count (each multiply has a collective at N > 1)."""
+    import torch
+    import torch.distributed as dist
+
+    t0 = time.perf_counter()
+    for _ in range(min_launches):
+        e.multiply()
+    e.sync()
+    per = (time.perf_counter() - t0) / max(1, min_launches)
+    more = int(min(2000, max(0.0, seconds / max(per, 1e-6) - min_launches)))
+    if distributed:
+        t = torch.tensor([float(more)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        more = int(t[0])
+    for _ in range(more):
+        e.multiply()
+    e.sync()
+
+
 def single_process_section(args, n, R, C, we_set_nccl_debug):
     """The drop-in executables' single-process form of the same workload: ONE process drives all
     N GPUs (mvg_comm_init_all -> ncclCommInitAll over N devices, the grouped ncclCommSplit and the
@@ -480,9 +506,7 @@ def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, tota
     steps = max(10, args.steps // 2)
 
     def run_exact():
-        for _ in range(max(2, args.warmup // 4)):
-            eng.multiply()
-        eng.sync()
+        warm(eng, max(2, args.warmup // 4), distributed, local)
         eng.kernel_timing(args.event_every)
         barrier()
         t0 = time.perf_counter()
@@ -717,9 +741,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
         e = mm.Multiplier(alg, R, C, comm)
         try:
             e.fill_synth()
-            for _ in range(3):
-                e.multiply()
-            e.sync()
+            warm(e, 3, distributed, local)
             el, kms = timed(e, args.config_steps)
             tree_by_rank = by_rank[0]
             y = e.collect()
@@ -730,9 +752,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
                 # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
                 # every partial to rank 0, the reference's combine order there)
                 e.set_exact(True)
-                for _ in range(2):
-                    e.multiply()
-                e.sync()
+                warm(e, 2, distributed, local)
                 xsteps = max(5, args.config_steps // 2)
                 xel, xkms = timed(e, xsteps)
                 yx = e.collect()

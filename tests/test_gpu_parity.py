@@ -56,6 +56,26 @@ def test_gemv_all_variants_vs_oracle(m, k):
         assert max_rel(y, y_ref) <= TOL, (name, m, k)
 
 
+@pytest.mark.parametrize("m,k", [(5, 7), (65, 127), (257, 1000), (33, 4096), (130, 16388), (2049, 512), (3, 65538)])
+def test_gemv_all_variants_on_signed_data(m, k):
+    """Mixed-sign inputs (cancellation): the relative bar per element is ill-conditioned there, so
+    the tree-summed kernels are held to the forward-error bound of a sum of k products,
+    |y - y_ref| <= 1e-13 * sum_j |a_ij x_j| per row (k * eps * sum|.| is 1.5e-12 at k = 65538; the
+    fixed-order tree does far better), against the reference's sequential sums (the oracle)."""
+    rng = np.random.default_rng(m * 7919 + k)
+    A = rng.uniform(-1.0, 1.0, size=(m, k))
+    x = rng.uniform(-1.0, 1.0, size=k)
+    y_ref = oracle.multiply_std_rowwise(A, x)
+    scale = np.abs(A) @ np.abs(x)
+    for v in range(_lib.lib.mvg_gemv_variant_count()):
+        name = _lib.lib.mvg_gemv_variant_name(v).decode()
+        y = mm.multiply_std_rowwise(A, x, variant=v)
+        err = float(np.max(np.abs(y - y_ref) / scale))
+        assert err <= 1e-13, (name, m, k, err)
+    # the exact kernels: the reference's own bits, signs or not
+    assert np.array_equal(mm.multiply_std_rowwise(A, x, exact=True), y_ref), (m, k)
+
+
 def test_gemv_16b_kernels_on_views_off_16b():
     # A and x starting 8 bytes into their buffers (an offset view), odd and even lda
     for m, k, lda in [(70, 300, 301), (130, 4096, 4097), (9, 20001, 20002), (257, 1000, 1000)]:
