@@ -32,6 +32,7 @@ connection and the communicator sizes, from its NCCL_DEBUG=INFO log) and `kernel
 from __future__ import annotations
 
 import argparse
+import gc
 import glob
 import json
 import os
@@ -243,6 +244,7 @@ def main():
     eng.sync()
 
     eng.kernel_timing(args.event_every)
+    gc.disable()  # no collector pause inside the timed region (K = 20 steps are 6 ms)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -250,6 +252,7 @@ def main():
     eng.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     kt = eng.kernel_ms()
     eng.kernel_timing(0)
 
