@@ -149,9 +149,21 @@ def relay(cmd: list[str], env: dict | None = None) -> int:
     be replaced after it has), pass its stderr through, print the one JSON line its rank 0 wrote
     on stdout (every other stdout line goes to stderr), and return its exit code (1 if it exited
     0 without a JSON line)."""
+    import signal
     import subprocess
 
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+
+    def forward(signum, _frame):  # a time limit on this process reaches the ranks too
+        p.send_signal(signum)
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
     line = None
     for ln in p.stdout:
         s = ln.strip()

@@ -102,6 +102,33 @@ def test_relay_prints_rank0_line_and_passes_the_exit_code(capsys):
     assert bench.relay(_child("print('no json here')")) == 1
 
 
+def test_relay_passes_a_termination_on_to_the_ranks(tmp_path):
+    """A time limit that terminates `bench.py --gpus N` must end the ranks it started too."""
+    import time
+
+    marker = tmp_path / "child_pid"
+    child_py, parent_py = tmp_path / "child.py", tmp_path / "parent.py"
+    child_py.write_text(f"import os, time\nopen({str(marker)!r}, 'w').write(str(os.getpid()))\ntime.sleep(60)\n")
+    parent_py.write_text(f"import sys\nsys.path.insert(0, {REPO!r})\nimport bench\n"
+                         f"bench.relay([sys.executable, {str(child_py)!r}])\n")
+    p = subprocess.Popen([sys.executable, str(parent_py)])
+    for _ in range(200):
+        if marker.exists() and marker.read_text():
+            break
+        time.sleep(0.1)
+    child = int(marker.read_text())
+    p.terminate()
+    assert p.wait(timeout=30) == 128 + 15
+    for _ in range(50):  # the child is gone (reaped by the parent's wait)
+        try:
+            os.kill(child, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("the relayed child outlived its terminated parent")
+
+
 def test_bench_without_launcher_starts_the_ranks_itself():
     """`python bench.py --gpus 2` with no WORLD_SIZE: bench.py runs torch.distributed.run itself as
     a child. Here (no GPU) the two ranks fail at their first GPU call, and that failure is the
