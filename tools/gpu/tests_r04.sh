@@ -3,7 +3,7 @@ set -o pipefail
 OUT=gpurun_out/${OUT:-t4a}
 mkdir -p $OUT
 echo "== sustained exact forms"
-timeout -k 10 300 python -u tools/probes/sustained_exact.py 16384 16384 100 > $OUT/sustained_16384.jsonl 2> $OUT/sustained.err || exit $?
+timeout -k 10 300 python -u tools/probes/exact_context_probe.py sustained 16384 16384 100 > $OUT/sustained_16384.jsonl 2> $OUT/sustained.err || exit $?
 echo "== pytest gpu"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
