@@ -449,7 +449,7 @@ def warm(e, min_launches, distributed, local, seconds=0.1):
     e.sync()
 
 
-def single_process_section(args, n, R, C, we_set_nccl_debug):
+def single_process_section(args, n, R, C, we_set_nccl_debug, exe=None):
     """The drop-in executables' single-process form of the same workload: ONE process drives all
     N GPUs (mvg_comm_init_all -> ncclCommInitAll over N devices, the grouped ncclCommSplit and the
     exchange grouped over the local devices, csrc/engine.cpp), which the one-rank-per-GPU
@@ -468,7 +468,7 @@ def single_process_section(args, n, R, C, we_set_nccl_debug):
     if have < n or os.environ.get("MVG_SAME_DEVICE") == "1":
         return {"ran": False, "why": f"needs {n} devices in one process, {have} visible"
                 + (" (MVG_SAME_DEVICE rehearsal: every rank on one GPU)" if os.environ.get("MVG_SAME_DEVICE") == "1" else "")}
-    exe = os.path.join(REPO, "bin", f"multiplier_{args.alg}")
+    exe = exe or os.path.join(REPO, "bin", f"multiplier_{args.alg}")
     if not os.access(exe, os.X_OK):
         return {"ran": False, "why": f"{os.path.relpath(exe, REPO)} not built"}
     work = tempfile.mkdtemp(prefix="mvg_single_")

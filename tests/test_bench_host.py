@@ -148,6 +148,41 @@ def test_single_process_section_needs_n_devices():
     assert r["ran"] is False and "needs 8 devices" in r["why"]
 
 
+def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path, monkeypatch):
+    """With N devices visible, rank 0 runs the executables' one-process-N-GPU form as a child and
+    records its device-resident line and y (here a stand-in executable on the CPU)."""
+    import torch
+
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.delenv("MVG_SAME_DEVICE", raising=False)
+    R, C = 64, 32
+    fake = tmp_path / "multiplier_colwise"
+    fake.write_text("#!/usr/bin/env python3\n"
+                    "import os, sys\n"
+                    "assert os.environ['MVG_NGPUS'] == '8' and os.environ['MVG_SYNTH'] == 'device'\n"
+                    "assert 'RANK' not in os.environ and sys.argv[1:] == ['64', '32']\n"
+                    "open(os.environ['MVG_Y_OUT'], 'w').write('1.5\\n' * 64)\n"
+                    "print('end-to-end (multiply + y on root; inputs generated on the GPUs, nothing distributed): mean 0.000100 s over 50 iterations')\n"
+                    "print('device-resident: 0.0500 ms per multiply, 123.4 GB/s aggregate; GEMV kernel 0.040 ms (max over GPUs)')\n")
+    fake.chmod(0o755)
+
+    class A:
+        alg = "colwise"
+    monkeypatch.setenv("RANK", "0")
+    r = bench.single_process_section(A(), 8, R, C, False, exe=str(fake))
+    assert r["ran"] and r["rc"] == 0, r
+    assert r["ms_per_step"] == 0.05 and r["value"] == 123.4 and r["kernel_ms"] == 0.04 and r["end_to_end_s"] == 0.0001
+    assert "reference_rows" not in r  # the column split's config-2 rows are not the weak-scaled row split's
+    # a failing executable is recorded (and counted as a failed check), never raised
+    bad = tmp_path / "bad"
+    bad.write_text("#!/bin/sh\necho boom >&2\nexit 3\n")
+    bad.chmod(0o755)
+    bench.FAILURES.clear()
+    r = bench.single_process_section(A(), 8, R, C, False, exe=str(bad))
+    assert r["rc"] == 3 and "boom" in r["error"] and len(bench.FAILURES) == 1
+    bench.FAILURES.clear()
+
+
 def test_kernel_family_names():
     assert bench.kernel_family("rowblk_w4_r2_u8") == "gemv_rowblock"
     assert bench.kernel_family("rowblk_w8_r2_u4_splitk") == "gemv_rowblock_split"
