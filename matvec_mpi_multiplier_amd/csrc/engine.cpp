@@ -491,7 +491,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         if (l.rank == 0)
             if ((rc = alloc_doubles(&s.dy, R)) != MVG_OK) return bail(rc);
         // Warm the device before any timed loop: first-touch every buffer (the first H2D into
-        // never-touched HBM ran at 11 GB/s instead of 56, tools/probes/numa_h2d.py) and launch the
+        // never-touched HBM ran at 11 GB/s instead of 56, profiles/r01/e2e_small/numa_h2d.jsonl) and launch the
         // shard's GEMV once (loads its code object and any split-K workspace). These one-time
         // costs are the GPU runtime's analogue of MPI_Init; without this they landed in the
         // executables' first timed iteration (+0.1 ms on the mean at 600 x 600).
