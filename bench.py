@@ -208,6 +208,7 @@ def main():
     # log to a file of their own (NCCL_DEBUG_FILE) keeps it untouched, and the report is skipped.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     rccl_log, caller_debug = None, os.environ.get("NCCL_DEBUG")
+    caller_nccl = {k: os.environ.get(k) for k in ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE")}
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG_FILE" not in os.environ:
         rccl_log = f"/tmp/mvg_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log"
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=rccl_log)
@@ -415,7 +416,7 @@ def main():
         if n > 1:
             # the executables' one-process-drives-N-GPUs path (ncclCommInitAll, grouped exchange),
             # which the rank-per-GPU sections above never run; the other ranks have exited
-            out["single_process"] = single_process_section(args, n, R, C, rccl_log is not None)
+            out["single_process"] = single_process_section(args, n, R, C, caller_nccl)
         out["failures"] = FAILURES or None
         json_out.write(json.dumps(out) + "\n")
         json_out.flush()
@@ -449,7 +450,7 @@ def warm(e, min_launches, distributed, local, seconds=0.1):
     e.sync()
 
 
-def single_process_section(args, n, R, C, we_set_nccl_debug, exe=None):
+def single_process_section(args, n, R, C, caller_nccl=None, exe=None):
     """The drop-in executables' single-process form of the same workload: ONE process drives all
     N GPUs (mvg_comm_init_all -> ncclCommInitAll over N devices, the grouped ncclCommSplit and the
     exchange grouped over the local devices, csrc/engine.cpp), which the one-rank-per-GPU
@@ -476,9 +477,11 @@ def single_process_section(args, n, R, C, we_set_nccl_debug, exe=None):
         ypath = os.path.join(work, "y.txt")
         drop = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
                 "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT"}
-        if we_set_nccl_debug:
-            drop |= {"NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE"}
         env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC")}
+        for k, v in (caller_nccl or {}).items():  # RCCL's logging as the caller set it, not ours
+            env.pop(k, None)
+            if v is not None:
+                env[k] = v
         iters = 50
         env.update(MVG_NGPUS=str(n), MVG_SYNTH="device", MVG_ITERS=str(iters), MVG_Y_OUT=ypath)
         cmd = [exe, str(R), str(C)]

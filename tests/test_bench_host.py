@@ -144,7 +144,7 @@ def test_bench_without_launcher_starts_the_ranks_itself():
 def test_single_process_section_needs_n_devices():
     class A:
         alg = "rowwise"
-    r = bench.single_process_section(A(), 8, 8 * 16384, 16384, False)
+    r = bench.single_process_section(A(), 8, 8 * 16384, 16384)
     assert r["ran"] is False and "needs 8 devices" in r["why"]
 
 
@@ -161,6 +161,7 @@ def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path,
                     "import os, sys\n"
                     "assert os.environ['MVG_NGPUS'] == '8' and os.environ['MVG_SYNTH'] == 'device'\n"
                     "assert 'RANK' not in os.environ and sys.argv[1:] == ['64', '32']\n"
+                    "assert os.environ.get('NCCL_DEBUG') == 'WARN' and 'NCCL_DEBUG_FILE' not in os.environ\n"
                     "open(os.environ['MVG_Y_OUT'], 'w').write('1.5\\n' * 64)\n"
                     "print('end-to-end (multiply + y on root; inputs generated on the GPUs, nothing distributed): mean 0.000100 s over 50 iterations')\n"
                     "print('device-resident: 0.0500 ms per multiply, 123.4 GB/s aggregate; GEMV kernel 0.040 ms (max over GPUs)')\n")
@@ -169,7 +170,8 @@ def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path,
     class A:
         alg = "colwise"
     monkeypatch.setenv("RANK", "0")
-    r = bench.single_process_section(A(), 8, R, C, False, exe=str(fake))
+    monkeypatch.setenv("NCCL_DEBUG", "INFO")  # what the bench sets for its own ranks
+    r = bench.single_process_section(A(), 8, R, C, {"NCCL_DEBUG": "WARN", "NCCL_DEBUG_FILE": None}, exe=str(fake))
     assert r["ran"] and r["rc"] == 0, r
     assert r["ms_per_step"] == 0.05 and r["value"] == 123.4 and r["kernel_ms"] == 0.04 and r["end_to_end_s"] == 0.0001
     assert "reference_rows" not in r  # the column split's config-2 rows are not the weak-scaled row split's
@@ -178,7 +180,7 @@ def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path,
     bad.write_text("#!/bin/sh\necho boom >&2\nexit 3\n")
     bad.chmod(0o755)
     bench.FAILURES.clear()
-    r = bench.single_process_section(A(), 8, R, C, False, exe=str(bad))
+    r = bench.single_process_section(A(), 8, R, C, None, exe=str(bad))
     assert r["rc"] == 3 and "boom" in r["error"] and len(bench.FAILURES) == 1
     bench.FAILURES.clear()
 
