@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--config-cpu-sample-bytes", type=float, default=3.5e10,
                     help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
     ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--config-e2e-bytes", type=float, default=17.2e9,
+                    help="configs whose A is at most this size also run the end-to-end loop (config 5, the "
+                         "tall-skinny one: 16 GiB)")
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-vector GEMV section")
     ap.add_argument("--no-loader", action="store_true", help="skip the text-loader section")
     ap.add_argument("--no-exact", action="store_true",
@@ -766,6 +769,12 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             yx = None
             if rank == 0:
                 expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range")
+            e2e = None
+            if not args.no_e2e and args.e2e_iters > 0 and 8 * R * C <= args.config_e2e_bytes:
+                # north_star's end-to-end time on the tall-skinny config too: the root's host A
+                # distributed over every GPU's link, multiplied, y on the root (same values as the
+                # device-resident fill, so the exact section below still multiplies the same A)
+                e2e = end_to_end(args, e, mm, R, C, rank, distributed, barrier, y, total, local)
             if not args.no_exact:
                 # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
                 # every partial to rank 0, the reference's combine order there)
@@ -798,6 +807,7 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
             "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
             "pmc": pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)),
             "exact": exact,
+            "end_to_end": e2e,
         }
         if rank == 0:
             entry["reference_rows"] = reference_rows_check(name, alg, R, C, n, y, yx)
