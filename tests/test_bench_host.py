@@ -1,6 +1,7 @@
 """bench.py's host-side helpers on the CPU (no GPU): the RCCL transport report parser, the
 reference-row check every config's y goes through, the launcher relay that lets `bench.py --gpus N`
-run without torch.distributed.run, the check recorder and the PMC summary lookup."""
+run without torch.distributed.run, the check recorder, the PMC summary lookup, the warm-up and
+the reference rank sweep."""
 import json
 import os
 import subprocess
@@ -206,3 +207,48 @@ def test_pmc_summary_finds_the_committed_counters():
     assert bench.pmc_summary(16384, 16384, "panel_l8_w2_u16 (column panels, P = 256)")["source"].endswith(
         "pmc_gemv_seq_hop_panel_16384x16384.json")
     assert bench.pmc_summary(3, 5, "rowblk_w4_r2_u8") is None
+
+
+def test_warm_runs_about_the_requested_time():
+    """warm(): at least `min_launches`, then enough more for ~`seconds` of multiplies."""
+    import time
+
+    class Eng:
+        calls = 0
+
+        def multiply(self):
+            Eng.calls += 1
+            time.sleep(0.001)
+
+        def sync(self):
+            pass
+
+    bench.warm(Eng(), 3, False, 0, seconds=0.03)
+    assert 3 <= Eng.calls and 20 <= Eng.calls <= 40, Eng.calls
+    Eng.calls = 0
+    bench.warm(Eng(), 5, False, 0, seconds=0.0)
+    assert Eng.calls == 5
+
+
+def test_ref_sweep_reports_speedup_and_efficiency(monkeypatch):
+    """cpu_baseline.sweep: S = T1 / TP and E = S / P (the reference's README.md:47-50), points that
+    do not split the sample skipped, a failing point recorded."""
+    from oracle import ref_runner
+
+    secs = {1: 0.050, 2: 0.030, 4: 0.020, 8: 0.025}
+
+    def fake_run(alg, R, C, p, timeout=None, cpus=None, rows=None):
+        if p == 8:
+            raise RuntimeError("mpiexec failed")
+        return {"seconds": secs[p], "y": None, "wall_s": 1.0}
+
+    monkeypatch.setattr(ref_runner, "run", fake_run)
+
+    class A:
+        ref_timeout = 10.0
+    out = bench.ref_sweep(A(), "rowwise", 1024, 16384, 16, 0.040, "compact", (1, 2, 4, 8, 3), 8 * 1024 * 16384)
+    pts = {p["P"]: p for p in out["points"]}
+    assert sorted(pts) == [1, 2, 4, 16]  # 3 does not split 1024 rows; 8 failed
+    assert pts[1]["speedup"] == 1.0 and pts[2]["speedup"] == round(0.05 / 0.03, 3)
+    assert pts[16]["efficiency"] == round(0.05 / 0.04 / 16, 3) and pts[16]["placement"] == "compact"
+    assert out["errors"] and "P=8" in out["errors"][0]
