@@ -1,14 +1,11 @@
-# Round-4 final check on one MI355X (gpurun, repo root): the exact-context probe, the GPU test
-# suite, smoke(), and the driver's N = 1 bench under rocprofv3's kernel trace. Output in
+# Round-4 final check on one MI355X (gpurun, repo root): the GPU test suite, smoke(), the
+# driver's N = 1 bench under rocprofv3's kernel trace, then the exact-context probe. Output in
 # gpurun_out/$OUT; each GPU step under its own time limit, the first failure ends the script.
 set -o pipefail
 OUT=gpurun_out/${OUT:-f4a}
 ROOT=$PWD
 mkdir -p $OUT
 export TMPDIR=/tmp
-echo "== exact context probe"
-timeout -k 10 150 python -u tools/probes/exact_context_probe.py engine 16384 16384 50 > $OUT/probe.jsonl 2> $OUT/probe.err || exit $?
-timeout -k 10 200 python -u tools/probes/exact_context_probe.py queues 16384 16384 30 >> $OUT/probe.jsonl 2>> $OUT/probe.err || exit $?
 echo "== pytest gpu"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
@@ -20,3 +17,6 @@ cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format cs
     python3 $ROOT/bench.py --steps 20 --warmup 5 > $ROOT/$OUT/bench.json 2> $ROOT/$OUT/bench.err || { tail $ROOT/$OUT/bench.err; exit 1; }
 cd $ROOT && python3 tools/rocprof_by_grid.py $OUT/prof --out $OUT/kernel_by_grid.csv
 tail -c 200 $OUT/bench.json
+echo "== exact context probe"
+timeout -k 10 150 python -u tools/probes/exact_context_probe.py engine 16384 16384 50 > $OUT/probe.jsonl 2> $OUT/probe.err || exit $?
+timeout -k 10 200 python -u tools/probes/exact_context_probe.py queues 16384 16384 30 >> $OUT/probe.jsonl 2>> $OUT/probe.err || exit $?
