@@ -316,19 +316,21 @@ __device__ __forceinline__ bool lines_aligned(const double* A, int64_t lda) {
 // (16384 x 16386: 373 us against 314 us at 16384^2, sweep_exact13_lines.jsonl) — then nseg
 // main segments, the same count for every row of the wave, then one or two tail segments for
 // what is left. Head and tails are masked segments (zeros outside the row's columns).
-template <int L, int W, int U, bool B8 = false>
-__global__ __launch_bounds__(64) void gemv_seq_hop(const double* __restrict__ A, int64_t lda,
-                                                   const double* __restrict__ x,
-                                                   double* __restrict__ y, int64_t M, int64_t K) {
+// NW waves per workgroup (wave w of workgroup b owns rows [(b * NW + w) * R, +R)): with NW > 1 and
+// a launch-time LDS reservation, the dispatcher places the same number of waves on every CU.
+template <int L, int W, int U, bool B8 = false, int NW = 1>
+__global__ __launch_bounds__(64 * NW) void gemv_seq_hop(const double* __restrict__ A, int64_t lda,
+                                                        const double* __restrict__ x,
+                                                        double* __restrict__ y, int64_t M, int64_t K) {
     static_assert(L == 1 || L == 2 || L == 4 || L == 8 || L == 16 || L == 32 || L == 64, "lanes per row");
     static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B pieces; segment pairs per unrolled step");
     constexpr int R = 64 / L;  // rows per wave
     constexpr int S = L * W;   // columns per segment
     constexpr int V = W / 2;   // 16-B pieces per lane per segment
     static_assert(S >= 16, "the head (up to 15 columns) fits one segment");
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int c = lane % L;
-    const int64_t row = (int64_t)blockIdx.x * R + lane / L;
+    const int64_t row = ((int64_t)blockIdx.x * NW + (threadIdx.x >> 6)) * R + lane / L;
     const int64_t rr = row < M ? row : M - 1;
     const double* arow = A + rr * lda;
     const int off[2] = {c * W, (L - 1 - c) * W};  // even / odd segment
@@ -656,6 +658,7 @@ struct SeqVariant {
     int rows;   // rows per workgroup
     int waves = 1;       // waves per workgroup
     bool xlds = false;   // x staged in LDS (K doubles of dynamic LDS; K <= kXlMaxK)
+    int lds_reserve = 0;  // dynamic LDS bytes reserved (unused by the kernel): workgroups per CU cap
 };
 
 // kVec16: 16-B loads, so 16-B aligned A and x and an even lda; kVec16Lda23: also 32-bit
@@ -664,6 +667,10 @@ constexpr int kAnyOperands = 0, kVec16 = 1, kVec16Lda23 = 2;
 #define SEQ(RW, T, NB) {"seq_r" #RW "_t" #T "_b" #NB, gemv_seq<RW, T, NB>, kVec16Lda23, RW}
 #define HOP(L, W, U) {"hop_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U>, kVec16, 64 / L}
 #define HOP8(L, W, U) {"hop8_l" #L "_w" #W "_u" #U, gemv_seq_hop<L, W, U, true>, kAnyOperands, 64 / L}
+// NW waves per workgroup and an LDS reservation that lets only 160 / KB of them on a CU: the
+// same count of long-lived waves on every CU
+#define HOP8E(L, W, U, NW, KB) \
+    {"hop8e_l" #L "_w" #W "_u" #U "_n" #NW, gemv_seq_hop<L, W, U, true, NW>, kAnyOperands, NW * 64 / L, NW, false, KB * 1024}
 #define HOPXL(L, W, U, NW) \
     {"hopxl_l" #L "_w" #W "_u" #U "_n" #NW, gemv_seq_hop_xl<L, W, U, NW>, kAnyOperands, NW * 64 / L, NW, true}
 static constexpr SeqVariant kSeqVariants[] = {
@@ -702,6 +709,9 @@ static constexpr SeqVariant kSeqVariants[] = {
     HOP8(16, 4, 8),
     HOP8(16, 8, 4),
     HOP8(32, 8, 4),
+    // the same waves placed evenly: one 8-wave workgroup per CU, or two 4-wave ones
+    HOP8E(8, 2, 16, 8, 96),
+    HOP8E(8, 2, 16, 4, 64),
     // x staged in LDS once per workgroup of NW waves (short rows)
     HOPXL(8, 2, 16, 4),
     HOPXL(8, 2, 8, 4),
@@ -847,7 +857,7 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         cap = cap / var.rows * var.rows;
         if (cap < max_rows) max_rows = cap;
     }
-    const size_t lds = var.xlds ? (size_t)k * sizeof(double) : 0;
+    const size_t lds = var.xlds ? (size_t)k * sizeof(double) : (size_t)var.lds_reserve;
     for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
         const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
         const int rw = var.rows;

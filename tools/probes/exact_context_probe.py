@@ -13,7 +13,10 @@ MODE
               with the GPU's clock, power and temperature after (rocm-smi), two passes in opposite
               orders;
   queues    : the tree and the exact kernel on the default stream and on 8 fresh streams (HIP maps
-              streams onto GPU_MAX_HW_QUEUES hardware queues round robin), interleaved twice.
+              streams onto GPU_MAX_HW_QUEUES hardware queues round robin), interleaved twice;
+  repeat    : the tree and the row-major exact variants (default placement, and the evenly placed
+              hop8e_* forms) timed 12 times each, interleaved, each time after 0.1 s of load: the
+              spread of one kernel's time from one burst to the next.
 One JSON line per measurement.
 """
 import ctypes as C
@@ -178,12 +181,39 @@ def mode_queues(M, K, n, nstreams=8):
               flush=True)
 
 
+def mode_repeat(M, K, n, reps=12):
+    s = torch.cuda.current_stream().cuda_stream
+    A, x, y = inputs(M, K, s)
+    forms = ["tree", "hop8_l8_w2_u16", "hop8e_l8_w2_u16_n8", "hop8e_l8_w2_u16_n4"]
+
+    def fn(form):
+        if form == "tree":
+            return lambda: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)
+        v = exact_variant(form)
+        return lambda: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, v, s)
+
+    res = {f: [] for f in forms}
+    heat = fn("tree")
+    for _ in range(reps):
+        for form in forms:
+            f = fn(form)
+            torch.cuda.synchronize()
+            for _ in range(int(0.1 / 300e-6)):
+                heat()
+            us = sorted(per_launch_us(f, n))
+            res[form].append(round(us[n // 2], 2))
+    for form, v in res.items():
+        srt = sorted(v)
+        print(json.dumps({"mode": "repeat", "M": M, "K": K, "form": form, "burst_medians_us": v,
+                          "min_us": srt[0], "median_us": srt[len(srt) // 2], "max_us": srt[-1]}), flush=True)
+
+
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "engine"
     M = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 16384
     n = int(sys.argv[4]) if len(sys.argv) > 4 else 50
-    {"engine": mode_engine, "sustained": mode_sustained, "queues": mode_queues}[mode](M, K, n)
+    {"engine": mode_engine, "sustained": mode_sustained, "queues": mode_queues, "repeat": mode_repeat}[mode](M, K, n)
 
 
 if __name__ == "__main__":
