@@ -14,6 +14,10 @@ MODE
               orders;
   queues    : the tree and the exact kernel on the default stream and on 8 fresh streams (HIP maps
               streams onto GPU_MAX_HW_QUEUES hardware queues round robin), interleaved twice;
+  isolate   : the raw exact kernel on torch buffers and the default stream, timed in bursts before
+              and after each step that builds up the engine's process state: two more HIP streams,
+              a page-locked host buffer with copies on them, an RCCL-less engine (mm.Multiplier),
+              its destruction;
   repeat    : the tree and the row-major exact variants (default placement, and the evenly placed
               hop8e_* forms) timed 12 times each, interleaved, each time after 0.1 s of load: the
               spread of one kernel's time from one burst to the next.
@@ -181,6 +185,52 @@ def mode_queues(M, K, n, nstreams=8):
               flush=True)
 
 
+def mode_isolate(M, K, n, reps=4):
+    s0 = torch.cuda.current_stream()
+    s = s0.cuda_stream
+    A, x, y = inputs(M, K, s)
+    hop = exact_variant("hop8_l8_w2_u16")
+    exact = lambda: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, hop, s)  # noqa: E731
+    tree = lambda: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)  # noqa: E731
+
+    def bursts(stage):
+        for kname, f in (("tree", tree), ("exact_hop8", exact)):
+            meds = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                for _ in range(int(0.1 / 300e-6)):
+                    tree()
+                us = sorted(per_launch_us(f, n))
+                meds.append(round(us[n // 2], 2))
+            print(json.dumps({"mode": "isolate", "M": M, "K": K, "stage": stage, "kernel": kname,
+                              "burst_medians_us": meds}), flush=True)
+
+    bursts("fresh process")
+    extra = [torch.cuda.Stream(device=DEV) for _ in range(2)]
+    for st in extra:  # used once each, as the engine's streams are
+        with torch.cuda.stream(st):
+            torch.empty(1024, device=DEV).fill_(1.0)
+    torch.cuda.synchronize()
+    bursts("+ two used streams")
+    h = torch.empty(1 << 19, dtype=torch.float64, pin_memory=True)
+    d = torch.empty(1 << 19, dtype=torch.float64, device=DEV)
+    for st in extra:
+        with torch.cuda.stream(st):
+            d.copy_(h, non_blocking=True)
+            h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    bursts("+ page-locked copies on them")
+    comm = mm.Comm.init_all([0])
+    eng = mm.Multiplier("rowwise", M, K, comm)
+    eng.fill_synth()
+    eng.sync()
+    bursts("+ an engine")
+    eng.destroy()
+    comm.destroy()
+    torch.cuda.synchronize()
+    bursts("engine destroyed")
+
+
 def mode_repeat(M, K, n, reps=12):
     s = torch.cuda.current_stream().cuda_stream
     A, x, y = inputs(M, K, s)
@@ -213,7 +263,8 @@ def main():
     M = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 16384
     n = int(sys.argv[4]) if len(sys.argv) > 4 else 50
-    {"engine": mode_engine, "sustained": mode_sustained, "queues": mode_queues, "repeat": mode_repeat}[mode](M, K, n)
+    {"engine": mode_engine, "sustained": mode_sustained, "queues": mode_queues, "repeat": mode_repeat,
+     "isolate": mode_isolate}[mode](M, K, n)
 
 
 if __name__ == "__main__":
