@@ -189,12 +189,13 @@ def mode_isolate(M, K, n, reps=4):
     s0 = torch.cuda.current_stream()
     s = s0.cuda_stream
     A, x, y = inputs(M, K, s)
-    hop = exact_variant("hop8_l8_w2_u16")
+    hop, hope = exact_variant("hop8_l8_w2_u16"), exact_variant("hop8e_l8_w2_u16_n8")
     exact = lambda: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, hop, s)  # noqa: E731
+    even = lambda: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, hope, s)  # noqa: E731
     tree = lambda: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)  # noqa: E731
 
     def bursts(stage):
-        for kname, f in (("tree", tree), ("exact_hop8", exact)):
+        for kname, f in (("tree", tree), ("exact_hop8", exact), ("exact_hop8e_n8", even)):
             meds = []
             for _ in range(reps):
                 torch.cuda.synchronize()
