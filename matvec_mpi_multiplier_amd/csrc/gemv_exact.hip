@@ -712,6 +712,7 @@ static constexpr SeqVariant kSeqVariants[] = {
     // the same waves placed evenly: one 8-wave workgroup per CU, or two 4-wave ones
     HOP8E(8, 2, 16, 8, 96),
     HOP8E(8, 2, 16, 4, 64),
+    HOP8E(8, 2, 24, 8, 96),
     // x staged in LDS once per workgroup of NW waves (short rows)
     HOPXL(8, 2, 16, 4),
     HOPXL(8, 2, 8, 4),

@@ -25,6 +25,9 @@ SHAPES = [
     ("cfg5_full_4194304x512", 4194304, 512),
     ("cfg3_g1_65536sq", 65536, 65536),
     ("mid_32768x16384", 32768, 16384),
+    ("cfg3_g4_strip_65536x16384", 65536, 16384),
+    ("mid_24576x16384", 24576, 16384),
+    ("mid_20480x16384", 20480, 16384),
     ("ref_4200sq", 4200, 4200),
     ("ref_10200sq", 10200, 10200),
     ("cfg4_full_131072sq", 131072, 131072),
