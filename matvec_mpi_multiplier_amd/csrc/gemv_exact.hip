@@ -33,6 +33,8 @@
 // 65536) the chain-hopping forms (gemv_seq_hop, below) take over: L lanes share a row, the data
 // arrives by plain coalesced loads into VGPRs, and the running sum hops from lane to lane by
 // DPP, still in column order.
+#include <atomic>
+
 #include "common.h"
 #include "lds_dma.h"
 
@@ -743,6 +745,11 @@ constexpr int kHopLongRows = seq_id(kSeqVariants, "hop8_l8_w2_u24");
 constexpr int kHopWide = seq_id(kSeqVariants, "hop8_l16_w4_u8");
 constexpr int kHopWidest = seq_id(kSeqVariants, "hop8_l16_w8_u4");
 constexpr int kHopFewRows = seq_id(kSeqVariants, "hop8_l32_w8_u4");
+constexpr int kHopEven = seq_id(kSeqVariants, "hop8e_l8_w2_u16_n8");
+constexpr int kHopEvenLong = seq_id(kSeqVariants, "hop8e_l8_w2_u24_n8");
+static_assert(kHopEven > 0 && kHopEvenLong > 0 && kSeqVariants[kHopEven].needs == kAnyOperands &&
+                  kSeqVariants[kHopEvenLong].needs == kAnyOperands,
+              "the evenly placed picks take any operands");
 static_assert(kSeqScalar > 0 && kSeqVariants[kSeqScalar].needs == kAnyOperands, "8-B exact fallback");
 static_assert(kSeqManyRows > 0 && kHopRows > 0 && kHopLongRows > 0 && kHopWide > 0 && kHopWidest > 0 &&
                   kHopFewRows > 0,
@@ -766,9 +773,45 @@ static_assert(kSeqVariants[kHopRows].needs == kAnyOperands && kSeqVariants[kHopL
 // R x 60000: 1200 rows in 203 us, 679 with the LDS forms), 16 x 32 B for short ones. On rows
 // that start mid-line they beat the tree form itself (16384 x 16386: 305 us against 315);
 // config 5's shards and 4,194,304 x 512 run at 0.96-1.0 of the tree form's speed.
+// short rows (K <= 768) go out in launches of at most 1 GiB of A (mvg_gemv_exact_variant below)
+constexpr int64_t kShortRowK = 768;
+constexpr int64_t kShortRowLaunchBytes = 1ll << 30;
+constexpr int64_t kMinPieceRows = 65536;
+constexpr int kMi355xCUs = 256;  // when no device answers (host-only callers, tests)
+//
+// Evenly placed 8-lane forms (round 4, profiles/r04/r4g, r4h): the 8-lane hop forms' one-wave
+// workgroups all stay resident for the whole launch, and how the dispatcher spreads them over the
+// CUs depends on the process's hardware-queue state — with two more used HIP streams in the
+// process (the engine's, torch's) the same launch took 335 us at 16384^2 against 312 alone. The
+// same waves as one 8-wave workgroup per CU (an LDS reservation admits one per CU) take 310-314 us
+// in every state, and 0.4-1.6 % less than the one-wave form in a fresh process (16384^2,
+// 16384 x 16383, 32768 x 16384, 65536^2). They are taken where whole rounds of one workgroup per
+// CU cover the rows (64-row workgroups a multiple of the CU count: the BASELINE configs' 16384-row
+// multiples); a partial last round costs a whole round (24576 x 16384: 541 against 470 us).
+static int device_cu_count() {
+    static std::atomic<int> cached[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return kMi355xCUs;
+    }
+    int n = cached[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = kMi355xCUs;
+    }
+    cached[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
+
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
     if (lines && operands_ok(kVec16Lda23, lda, aligned) && M >= 32768 && K > 2048 && K < 65536)
         return kSeqManyRows;
+    if (M >= 6144 && K > kShortRowK) {
+        const int64_t wgs = (M + 63) / 64, cus = device_cu_count();
+        if (wgs >= cus && wgs % cus == 0) return K >= 65536 ? kHopEvenLong : kHopEven;
+    }
     if (M >= 6144) return K >= 65536 ? kHopLongRows : kHopRows;
     if (M >= 2048) return K <= 8192 ? kHopRows : M < 4096 && K >= 32768 ? kHopWidest : kHopWide;
     return K <= 4096 ? kHopWide : kHopFewRows;
@@ -798,9 +841,6 @@ constexpr int kPanelRows = seq_id(kPanelVariants, "panel_l8_w2_u8");
 static_assert(kPanelRows > 0, "panel dispatch names a missing variant");
 constexpr int64_t kPanelWidth = 256;
 
-constexpr int64_t kShortRowK = 768;
-constexpr int64_t kShortRowLaunchBytes = 1ll << 30;
-constexpr int64_t kMinPieceRows = 65536;
 
 // one form for every shape: 24 segments in flight gained only 1-2 % from 32768 rows (round 2),
 // inside the box-to-box spread, so round 3 dropped that threshold
