@@ -714,7 +714,6 @@ static constexpr SeqVariant kSeqVariants[] = {
     // the same waves placed evenly: one 8-wave workgroup per CU, or two 4-wave ones
     HOP8E(8, 2, 16, 8, 96),
     HOP8E(8, 2, 16, 4, 64),
-    HOP8E(8, 2, 24, 8, 96),
     // x staged in LDS once per workgroup of NW waves (short rows)
     HOPXL(8, 2, 16, 4),
     HOPXL(8, 2, 8, 4),
@@ -746,10 +745,7 @@ constexpr int kHopWide = seq_id(kSeqVariants, "hop8_l16_w4_u8");
 constexpr int kHopWidest = seq_id(kSeqVariants, "hop8_l16_w8_u4");
 constexpr int kHopFewRows = seq_id(kSeqVariants, "hop8_l32_w8_u4");
 constexpr int kHopEven = seq_id(kSeqVariants, "hop8e_l8_w2_u16_n8");
-constexpr int kHopEvenLong = seq_id(kSeqVariants, "hop8e_l8_w2_u24_n8");
-static_assert(kHopEven > 0 && kHopEvenLong > 0 && kSeqVariants[kHopEven].needs == kAnyOperands &&
-                  kSeqVariants[kHopEvenLong].needs == kAnyOperands,
-              "the evenly placed picks take any operands");
+static_assert(kHopEven > 0 && kSeqVariants[kHopEven].needs == kAnyOperands, "the evenly placed pick takes any operands");
 static_assert(kSeqScalar > 0 && kSeqVariants[kSeqScalar].needs == kAnyOperands, "8-B exact fallback");
 static_assert(kSeqManyRows > 0 && kHopRows > 0 && kHopLongRows > 0 && kHopWide > 0 && kHopWidest > 0 &&
                   kHopFewRows > 0,
@@ -785,9 +781,10 @@ constexpr int kMi355xCUs = 256;  // when no device answers (host-only callers, t
 // process (the engine's, torch's) the same launch took 335 us at 16384^2 against 312 alone. The
 // same waves as one 8-wave workgroup per CU (an LDS reservation admits one per CU) take 310-314 us
 // in every state, and 0.4-1.6 % less than the one-wave form in a fresh process (16384^2,
-// 16384 x 16383, 32768 x 16384, 65536^2). They are taken where whole rounds of one workgroup per
-// CU cover the rows (64-row workgroups a multiple of the CU count: the BASELINE configs' 16384-row
-// multiples); a partial last round costs a whole round (24576 x 16384: 541 against 470 us).
+// 16384 x 16383, 32768 x 16384). They are taken where whole rounds of one workgroup per CU cover
+// the rows (64-row workgroups a multiple of the CU count: the BASELINE configs' 16384-row
+// multiples) and K < 65536; a partial last round costs a whole round (24576 x 16384: 541 against
+// 470 us), and at 131072^2 the 24-segment one-wave form stays 2 % ahead (19.64 against 20.03 ms).
 static int device_cu_count() {
     static std::atomic<int> cached[64];
     int dev = 0;
@@ -808,9 +805,9 @@ static int device_cu_count() {
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
     if (lines && operands_ok(kVec16Lda23, lda, aligned) && M >= 32768 && K > 2048 && K < 65536)
         return kSeqManyRows;
-    if (M >= 6144 && K > kShortRowK) {
+    if (M >= 6144 && K > kShortRowK && K < 65536) {
         const int64_t wgs = (M + 63) / 64, cus = device_cu_count();
-        if (wgs >= cus && wgs % cus == 0) return K >= 65536 ? kHopEvenLong : kHopEven;
+        if (wgs >= cus && wgs % cus == 0) return kHopEven;
     }
     if (M >= 6144) return K >= 65536 ? kHopLongRows : kHopRows;
     if (M >= 2048) return K <= 8192 ? kHopRows : M < 4096 && K >= 32768 ? kHopWidest : kHopWide;
