@@ -193,9 +193,20 @@ def mode_isolate(M, K, n, reps=4):
     exact = lambda: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, hop, s)  # noqa: E731
     even = lambda: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, hope, s)  # noqa: E731
     tree = lambda: lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s)  # noqa: E731
+    P = 256
+    Ap = torch.empty(M * P * (-(-K // P)), dtype=torch.float64, device=DEV)
+    check(lib.mvg_panel_relayout(A.data_ptr(), K, M, K, Ap.data_ptr(), M * P, P, s), "relayout")
+    pnames = [lib.mvg_gemv_exact_panel_variant_name(v).decode() for v in range(lib.mvg_gemv_exact_panel_variant_count())]
+
+    def panel(name):
+        v = pnames.index(name)
+        return lambda: lib.mvg_gemv_exact_panels(Ap.data_ptr(), M * P, P, x.data_ptr(), y.data_ptr(), M, K, v, s)
+
+    kernels = [("tree", tree), ("exact_hop8", exact), ("exact_hop8e_n8", even)]
+    kernels += [(n, panel(n)) for n in ("panel_l8_w2_u8", "panele_l8_w2_u8_n8", "panele_l8_w2_u16_n8") if n in pnames]
 
     def bursts(stage):
-        for kname, f in (("tree", tree), ("exact_hop8", exact), ("exact_hop8e_n8", even)):
+        for kname, f in kernels:
             meds = []
             for _ in range(reps):
                 torch.cuda.synchronize()
