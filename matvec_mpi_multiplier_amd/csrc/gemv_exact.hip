@@ -479,19 +479,21 @@ constexpr int64_t kXlMaxK = 8192;  // x in LDS: up to 64 KiB per workgroup
 // bit for bit. P is a power of two and a multiple of the segment (L*W columns), so no segment
 // straddles two panels; K % (L*W) columns end in one masked segment. Ap 16-B aligned with
 // P*8 a multiple of 128 B puts every segment on a cache line (no head segment).
-// NW waves per workgroup: as gemv_seq_hop's evenly placed forms (one 8-wave workgroup per CU)
-template <int L, int W, int U, int NW = 1>
-__global__ __launch_bounds__(64 * NW) void gemv_seq_hop_panel(const double* __restrict__ Ap, int64_t pstride, int lp,
-                                                              const double* __restrict__ x,
-                                                              double* __restrict__ y, int64_t M, int64_t K) {
+// (one-wave workgroups: unlike the row-major hop form's, their placement costs nothing
+// measurable — 299-302 us at 16384^2 in every process state; as 8-wave workgroups one per CU,
+// 304-309, round 4, profiles/r04/r4j)
+template <int L, int W, int U>
+__global__ __launch_bounds__(64) void gemv_seq_hop_panel(const double* __restrict__ Ap, int64_t pstride, int lp,
+                                                         const double* __restrict__ x,
+                                                         double* __restrict__ y, int64_t M, int64_t K) {
     static_assert(L == 8 || L == 16, "lanes per row");
     static_assert(W % 2 == 0 && U % 2 == 0, "whole 16-B pieces; segment pairs per unrolled step");
     constexpr int R = 64 / L;  // rows per wave
     constexpr int S = L * W;   // columns per segment
     constexpr int V = W / 2;   // 16-B pieces per lane per segment
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x;
     const int c = lane % L;
-    const int64_t row = ((int64_t)blockIdx.x * NW + (threadIdx.x >> 6)) * R + lane / L;
+    const int64_t row = (int64_t)blockIdx.x * R + lane / L;
     const int64_t rr = row < M ? row : M - 1;
     const int64_t pmask = (1ll << lp) - 1;
     const double* arow = Ap + (rr << lp);
@@ -822,25 +824,18 @@ typedef void (*panel_fn)(const double*, int64_t, int, const double*, double*, in
 struct PanelVariant {
     const char* name;
     panel_fn fn;
-    int rows;  // rows per workgroup
+    int rows;  // rows per one-wave workgroup
     int seg;   // columns per segment (P must be a multiple)
-    int waves = 1;        // waves per workgroup
-    int lds_reserve = 0;  // dynamic LDS bytes reserved: workgroups per CU cap
 };
 #define PANEL(L, W, U) {"panel_l" #L "_w" #W "_u" #U, gemv_seq_hop_panel<L, W, U>, 64 / L, L * W}
-#define PANELE(L, W, U, NW, KB) \
-    {"panele_l" #L "_w" #W "_u" #U "_n" #NW, gemv_seq_hop_panel<L, W, U, NW>, NW * 64 / L, L * W, NW, KB * 1024}
 static constexpr PanelVariant kPanelVariants[] = {
     {"auto", nullptr, 8, 16},  // 0
     PANEL(8, 2, 8),
     PANEL(8, 2, 16),
     PANEL(8, 2, 24),
     PANEL(16, 2, 16),
-    PANELE(8, 2, 8, 8, 96),
-    PANELE(8, 2, 16, 8, 96),
 };
 #undef PANEL
-#undef PANELE
 constexpr int kNumPanelVariants = (int)(sizeof(kPanelVariants) / sizeof(kPanelVariants[0]));
 constexpr int kPanelRows = seq_id(kPanelVariants, "panel_l8_w2_u8");
 static_assert(kPanelRows > 0, "panel dispatch names a missing variant");
@@ -985,12 +980,11 @@ int mvg_gemv_exact_panels(const double* Ap, int64_t pstride, int64_t P, const do
             return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: A and x must be 16-B aligned");
         if (pstride < m * P && (k + P - 1) / P > 1) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: pstride < m * P");
     }
-    const PanelVariant& var = kPanelVariants[v];
-    const int rw = var.rows;
+    const int rw = kPanelVariants[v].rows;
     const int64_t blocks = (m + rw - 1) / rw;
     if (blocks >= (1ll << 31)) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: too many rows for one launch");
-    hipLaunchKernelGGL(var.fn, dim3((unsigned)blocks), dim3(64 * var.waves), (size_t)var.lds_reserve,
-                       (hipStream_t)stream, Ap, pstride, lp, x, y, m, k);
+    hipLaunchKernelGGL(kPanelVariants[v].fn, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, Ap, pstride, lp,
+                       x, y, m, k);
     MVG_HIP(hipGetLastError());
     return MVG_OK;
 }
