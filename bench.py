@@ -429,12 +429,10 @@ def main():
 
 def warm(e, min_launches, distributed, local, seconds=0.1):
     """Untimed multiplies before a supplementary timed section: at least `min_launches`, and about
-    `seconds` of them, so that the section is timed at the clock a sustained run holds. The host
-    work between sections (y checks, D2H copies) idles the GPU long enough for it to drop its
-    clock, and the first milliseconds after that run slow; the memory-bound tree kernel does not
-    notice, the exact kernels (chain-paced, VALU busy 0.37-0.44) do (round 4: the row-major exact
-    form's first launches of a section 326-364 us against 313 us held). Every rank runs the same
-    count (each multiply has a collective at N > 1)."""
+    `seconds` of them, so that the section is timed in a steady state rather than right after the
+    host work between sections (y checks, D2H copies) has idled the GPU: the first launches after
+    such a gap run slow (round 4 traces: the tree kernel's first launch after a 16 ms gap 322 us,
+    then 300). Every rank runs the same count (each multiply has a collective at N > 1)."""
     import torch
     import torch.distributed as dist
 
