@@ -17,6 +17,9 @@ cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format cs
     python3 $ROOT/bench.py --steps 20 --warmup 5 > $ROOT/$OUT/bench.json 2> $ROOT/$OUT/bench.err || { tail $ROOT/$OUT/bench.err; exit 1; }
 cd $ROOT && python3 tools/rocprof_by_grid.py $OUT/prof --out $OUT/kernel_by_grid.csv
 tail -c 200 $OUT/bench.json
+echo "== bench N=1, the driver's command untraced"
+timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_untraced.json 2> $OUT/bench_untraced.err || { tail $OUT/bench_untraced.err; exit 1; }
+tail -c 200 $OUT/bench_untraced.json
 echo "== exact context probe"
 timeout -k 10 150 python -u tools/probes/exact_context_probe.py engine 16384 16384 50 > $OUT/probe.jsonl 2> $OUT/probe.err || exit $?
 timeout -k 10 200 python -u tools/probes/exact_context_probe.py queues 16384 16384 30 >> $OUT/probe.jsonl 2>> $OUT/probe.err || exit $?
