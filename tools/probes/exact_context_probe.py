@@ -17,7 +17,7 @@ MODE
   isolate   : the raw exact kernel on torch buffers and the default stream, timed in bursts before
               and after each step that builds up the engine's process state: two more HIP streams,
               a page-locked host buffer with copies on them, an RCCL-less engine (mm.Multiplier),
-              its destruction;
+              its destruction (PROBE_EXACT_VARIANTS=a,b adds exact variants by name);
   repeat    : the tree and the row-major exact variants (default placement, and the evenly placed
               hop8e_* forms) timed 12 times each, interleaved, each time after 0.1 s of load: the
               spread of one kernel's time from one burst to the next.
@@ -203,7 +203,10 @@ def mode_isolate(M, K, n, reps=4):
         return lambda: lib.mvg_gemv_exact_panels(Ap.data_ptr(), M * P, P, x.data_ptr(), y.data_ptr(), M, K, v, s)
 
     kernels = [("tree", tree), ("exact_hop8", exact), ("exact_hop8e_n8", even)]
-    kernels += [(n, panel(n)) for n in ("panel_l8_w2_u8", "panele_l8_w2_u8_n8", "panele_l8_w2_u16_n8") if n in pnames]
+    for name in filter(None, os.environ.get("PROBE_EXACT_VARIANTS", "").split(",")):
+        v = exact_variant(name)
+        kernels.append((name, lambda v=v: lib.mvg_gemv_exact_variant(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, v, s)))
+    kernels += [(n, panel(n)) for n in ("panel_l8_w2_u8",) if n in pnames]
 
     def bursts(stage):
         for kname, f in kernels:
