@@ -444,3 +444,22 @@ def test_multi_vector_dispatch_takes_dma_forms_on_long_rows():
     # 9..16 vectors: one pass on the matrix cores where the DMA forms run
     assert name(16384, 16384, 16) == name(8192, 1024, 9) == "m16_r2_t16_b2_w4_s5"
     assert not name(4200, 4200, 16).startswith("m16")
+
+
+def test_exact_row_major_dispatch():
+    """pick_seq_variant (host logic; with no GPU the CU count is the MI355X's 256): the LDS form for
+    line-aligned tall rows, the evenly placed 8-lane form where whole rounds of one 8-wave
+    workgroup per CU cover the rows (16384·k rows, 768 < K < 65536), the one-wave 8-lane forms
+    otherwise (partial rounds, short rows, K >= 65536), wider lane groups for few rows."""
+    name = lambda m, k, lda=None: _lib.lib.mvg_gemv_exact_variant_name(  # noqa: E731
+        _lib.lib.mvg_gemv_exact_auto_variant(lda or k, m, k)).decode()
+    assert name(16384, 16384) == "hop8e_l8_w2_u16_n8"     # config 2 (and its weak-scaled shards)
+    assert name(16384, 16383) == "hop8e_l8_w2_u16_n8"     # odd width, same rows
+    assert name(32768, 16384, 16386) == "hop8e_l8_w2_u16_n8"  # rows off the lines: no LDS form
+    assert name(32768, 16384) == "seqx_r64_t16_b2_g8"     # line-aligned tall rows: the LDS form
+    assert name(24576, 16384) == "hop8_l8_w2_u16"         # 1.5 rounds: a partial round costs a whole one
+    assert name(65536, 65536) == "hop8_l8_w2_u24"         # K >= 65536
+    assert name(131072, 131072) == "hop8_l8_w2_u24"
+    assert name(524288, 512) == "hop8_l8_w2_u16"          # short rows want more waves per CU
+    assert name(4194304, 512) == "hop8_l8_w2_u16"
+    assert name(1200, 60000).startswith("hop8_l32")       # few long rows: the chain dominates
