@@ -904,7 +904,12 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         const int rw = var.rows;
         hipLaunchKernelGGL(var.fn, dim3((unsigned)((mm + rw - 1) / rw)), dim3(64 * var.waves), lds, s,
                            A ? A + r0 * lda : A, lda, x, y + r0, mm, k);
-        MVG_HIP(hipGetLastError());
+        const hipError_t e = hipGetLastError();
+        // a runtime that refuses the evenly placed form's LDS reservation gets the same sums from
+        // the one-wave form (the whole call: nothing of it has been launched yet)
+        if (e != hipSuccess && variant == 0 && v == kHopEven && r0 == 0)
+            return mvg_gemv_exact_variant(A, lda, x, y, m, k, kHopRows, stream);
+        MVG_HIP(e);
     }
     return MVG_OK;
 }
