@@ -176,13 +176,19 @@ def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path,
     assert r["ran"] and r["rc"] == 0, r
     assert r["ms_per_step"] == 0.05 and r["value"] == 123.4 and r["kernel_ms"] == 0.04 and r["end_to_end_s"] == 0.0001
     assert "reference_rows" not in r  # the column split's config-2 rows are not the weak-scaled row split's
-    # a failing executable is recorded (and counted as a failed check), never raised
+    # a failing executable is recorded, never raised and not counted as a failed check (the
+    # scaling line's exit code stays 0); a wrong y from a run that finished is counted
     bad = tmp_path / "bad"
     bad.write_text("#!/bin/sh\necho boom >&2\nexit 3\n")
     bad.chmod(0o755)
     bench.FAILURES.clear()
     r = bench.single_process_section(A(), 8, R, C, None, exe=str(bad))
-    assert r["rc"] == 3 and "boom" in r["error"] and len(bench.FAILURES) == 1
+    assert r["rc"] == 3 and "boom" in r["error"] and bench.FAILURES == []
+    short = tmp_path / "multiplier_short"
+    short.write_text(fake.read_text().replace("* 64", "* 63"))
+    short.chmod(0o755)
+    r = bench.single_process_section(A(), 8, R, C, {"NCCL_DEBUG": "WARN", "NCCL_DEBUG_FILE": None}, exe=str(short))
+    assert r["rc"] == 0 and len(bench.FAILURES) == 1 and "63" in bench.FAILURES[0]
     bench.FAILURES.clear()
 
 
