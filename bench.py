@@ -28,24 +28,36 @@ the engine's column-panel copy, and `row_major`, the kernels a fresh distributio
 rate and kernel roofline fraction, and (rank 0, N = 1, row split) its y compared bit for bit with
 the oracle port's and the real reference's. At N > 1: `rccl` (the transport RCCL chose for every
 connection and the communicator sizes, from its NCCL_DEBUG=INFO log) and `kernel_ms_by_rank`.
+
+Wall-time budget (--budget-s): the headline is timed first; every section after it first checks
+that its estimated time fits in what is left of the budget (at N > 1 the decision is all-reduced,
+so every rank skips the same sections) and is recorded as {"skipped": "budget", ...} when it does
+not. `sections_s` holds each section's wall time. If rank 0 receives SIGTERM / SIGINT (a time
+limit around the run), it writes the line it has so far, marked "truncated": true, and exits.
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import gc
 import glob
 import json
 import os
+import signal
 import sys
+import threading
 import time
 
 import numpy as np
+
+T_START = time.perf_counter()  # the budget counts from here (imports included)
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 SHARD = 16384  # rows per GPU and columns (config 2)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "fp64 GEMV achieved HBM GB/s per GPU + end-to-end time at 1/2/4/8 MI355X"
 
 
 def parse():
@@ -83,9 +95,12 @@ def parse():
     ap.add_argument("--config-cpu-sample-bytes", type=float, default=3.5e10,
                     help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
     ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
-    ap.add_argument("--config-e2e-bytes", type=float, default=17.2e9,
-                    help="configs whose A is at most this size also run the end-to-end loop (config 5, the "
-                         "tall-skinny one: 16 GiB)")
+    ap.add_argument("--config-e2e", default="3,4,5",
+                    help="configs that also run the end-to-end loop, wherever host memory (and /dev/shm at "
+                         "N > 1) holds their A, measured at run time; '' for none")
+    ap.add_argument("--budget-s", type=float, default=420.0,
+                    help="wall-time budget of the whole run (about 70 %% of the driver's 600 s limit): a "
+                         "section whose estimate no longer fits is skipped and marked")
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-vector GEMV section")
     ap.add_argument("--no-loader", action="store_true", help="skip the text-loader section")
     ap.add_argument("--no-exact", action="store_true",
@@ -98,6 +113,138 @@ def log(*a):
 
 
 FAILURES: list[str] = []  # the bench's parity checks that failed (JSON `failures`; exit code 1)
+WARNINGS: list[str] = []  # product paths that ran and failed without failing a check (JSON `warnings`)
+
+
+class Budget:
+    """The run's wall-time budget, counted from the start of the process (T_START). `run(name,
+    need_s, fn, ...)` runs a section only when its estimate fits in what is left — at N > 1 the
+    answer is all-reduced (MIN), so every rank takes the same sections and no rank waits in a
+    collective another one skipped — and records its wall time in `sections`; a section that does
+    not fit returns a skip marker instead. `current` names the section in progress (a truncated
+    line says where the run was)."""
+
+    def __init__(self, limit_s: float, distributed: bool = False, device=None):
+        self.limit_s = float(limit_s)
+        self.distributed = distributed
+        self.device = device
+        self.sections: dict[str, float] = {}
+        self.skipped: list[str] = []
+        self.current: str | None = None
+
+    def used(self) -> float:
+        return time.perf_counter() - T_START
+
+    def left(self) -> float:
+        return self.limit_s - self.used()
+
+    def fits(self, need_s: float, collective: bool = True) -> bool:
+        ok = self.left() >= need_s
+        if self.distributed and collective:
+            import torch
+            import torch.distributed as dist
+
+            t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = float(t[0]) >= 1.0
+        return ok
+
+    def marker(self, need_s: float) -> dict:
+        return {"skipped": "budget", "need_s": round(need_s, 1), "left_s": round(self.left(), 1)}
+
+    def run(self, name: str, need_s: float, fn, *a, collective: bool = True):
+        if not self.fits(need_s, collective):
+            self.skipped.append(name)
+            log(f"bench: section {name} skipped: needs ~{need_s:.0f} s, {self.left():.0f} s of the budget left")
+            return self.marker(need_s)
+        t0, prev = time.perf_counter(), self.current
+        self.current = name
+        try:
+            return fn(*a)
+        finally:
+            self.sections[name] = round(time.perf_counter() - t0, 2)
+            self.current = prev
+
+    def record(self) -> dict:
+        return {"limit_s": self.limit_s, "used_s": round(self.used(), 1), "skipped": list(self.skipped)}
+
+
+class Report:
+    """Rank 0's JSON line under construction. Sections store their results as they finish;
+    `write()` prints the line once — at the end, or from the signal watcher when a time limit
+    terminates the run (`truncated`: the line as far as it got). The watcher is a thread woken
+    through signal.set_wakeup_fd, so the line goes out even while the main thread is blocked in a
+    GPU or C call that would delay a Python-level handler; it then ends the process with
+    os._exit (never an exec)."""
+
+    def __init__(self, stream, budget: Budget | None = None):
+        self.stream = stream
+        self.budget = budget
+        self.lock = threading.Lock()
+        self.out: dict = {}
+        self.written = False
+
+    def __setitem__(self, key, value):
+        with self.lock:
+            self.out[key] = value
+
+    def __getitem__(self, key):
+        with self.lock:
+            return self.out[key]
+
+    def update(self, d: dict) -> None:
+        with self.lock:
+            self.out.update(d)
+
+    def append(self, key, value) -> None:
+        with self.lock:
+            self.out.setdefault(key, []).append(value)
+
+    def snapshot(self, **extra) -> dict:
+        with self.lock:
+            line = copy.deepcopy(self.out)
+        if self.budget is not None:
+            line["sections_s"] = dict(self.budget.sections)
+            line["budget"] = self.budget.record()
+        line["failures"] = list(FAILURES) or None
+        line["warnings"] = list(WARNINGS) or None
+        line.update(extra)
+        return line
+
+    def write(self, **extra) -> bool:
+        line = self.snapshot(**extra)
+        with self.lock:
+            if self.written:
+                return False
+            self.written = True
+            self.stream.write(json.dumps(line) + "\n")
+            self.stream.flush()
+        return True
+
+    def watch_signals(self, exit_fn=None) -> None:
+        """SIGTERM / SIGINT: write the line so far (truncated) and exit 128 + signal."""
+        exit_fn = exit_fn or os._exit
+        rfd, wfd = os.pipe()
+        os.set_blocking(wfd, False)
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            signal.signal(sig, lambda *_: None)  # installs CPython's C handler; the watcher acts
+        signal.set_wakeup_fd(wfd, warn_on_full_buffer=False)
+
+        def watcher():
+            while True:
+                b = os.read(rfd, 1)
+                if not b:
+                    return
+                if b[0] not in (signal.SIGTERM, signal.SIGINT):
+                    continue
+                name = signal.Signals(b[0]).name
+                where = self.budget.current if self.budget is not None else None
+                log(f"bench: {name} during {where or 'the run'}: writing the line so far")
+                self.write(truncated=True, truncated_by=name, truncated_in=where)
+                exit_fn(128 + b[0])
+                return
+
+        threading.Thread(target=watcher, name="bench-signal-watcher", daemon=True).start()
 
 
 def expect(cond, msg) -> bool:
@@ -111,9 +258,12 @@ def expect(cond, msg) -> bool:
 
 
 def kernel_family(variant: str) -> str:
-    """The kernel template a dispatch variant name instantiates (the PMC summaries' key)."""
+    """The kernel template a dispatch variant name instantiates (the PMC summaries' key); the
+    evenly placed multi-wave hop forms (hop8e_*) are a family of their own, so they never take
+    counters recorded on the one-wave form."""
     for prefix, fam in (("rowlines", "gemv_rowblock_lines"), ("rowblk", "gemv_rowblock"), ("vec", "gemv_vec"),
-                        ("scl", "gemv_scalar"), ("hopxl", "gemv_seq_hop_xl"), ("hop", "gemv_seq_hop"),
+                        ("scl", "gemv_scalar"), ("hopxl", "gemv_seq_hop_xl"), ("hop8e", "gemv_seq_hop_n8"),
+                        ("hop", "gemv_seq_hop"),
                         ("seqx", "gemv_seq_x"), ("seq_", "gemv_seq"), ("panel", "gemv_seq_hop_panel")):
         if variant.startswith(prefix):
             return fam + ("_split" if variant.endswith("_splitk") else "")
@@ -152,32 +302,44 @@ def relay(cmd: list[str], env: dict | None = None) -> int:
     be replaced after it has), pass its stderr through, print the one JSON line its rank 0 wrote
     on stdout (every other stdout line goes to stderr), and return its exit code (1 if it exited
     0 without a JSON line)."""
-    import signal
     import subprocess
 
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    got: dict = {"line": None}
 
-    def forward(signum, _frame):  # a time limit on this process reaches the ranks too
+    def read():  # a thread, so a signal handler never re-enters the pipe's reader
+        for ln in p.stdout:
+            s = ln.strip()
+            if s.startswith("{") and '"metric"' in s:
+                got["line"] = s
+            elif s:
+                print(s, file=sys.stderr, flush=True)
+
+    reader = threading.Thread(target=read, daemon=True)
+    reader.start()
+
+    def forward(signum, _frame):
+        # a time limit on this process reaches the ranks too; rank 0 then writes its line so far
+        # (truncated), which is passed on before this process exits
         p.send_signal(signum)
         try:
-            p.wait(timeout=20)
+            p.wait(timeout=40)
         except subprocess.TimeoutExpired:
             p.kill()
+        reader.join(timeout=10)
+        if got["line"] is not None:
+            print(got["line"], flush=True)
         sys.exit(128 + signum)
 
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, forward)
-    line = None
-    for ln in p.stdout:
-        s = ln.strip()
-        if s.startswith("{") and '"metric"' in s:
-            line = s
-        elif s:
-            print(s, file=sys.stderr, flush=True)
-    rc = p.wait()
-    if line is not None:
-        print(line, flush=True)
-    if rc == 0 and line is None:
+    while p.poll() is None:  # never blocked inside Popen.wait, whose lock forward() needs
+        time.sleep(0.1)
+    rc = p.returncode
+    reader.join()
+    if got["line"] is not None:
+        print(got["line"], flush=True)
+    if rc == 0 and got["line"] is None:
         log("bench: the ranks exited without a JSON line")
         return 1
     return rc
@@ -202,6 +364,20 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = args.gpus
+    budget = Budget(args.budget_s)
+    report = Report(json_out, budget)
+    if rank == 0:
+        # from here on a time limit still gets a line: the fields known so far, "truncated": true
+        report.update({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n, "steps": args.steps,
+                       "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                       "dtype": "f64",
+                       "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text "
+                               "inputs)"})
+        report.watch_signals()
     # one process per GPU: CUDA-tensor / RCCL IPC between processes needs the dmabuf IPC mode on
     # this ROCm (the legacy handle path fails with hipIpcGetMemHandle: invalid argument); set before
     # the HIP runtime starts. With N > 1, RCCL logs at INFO to a per-rank file that rccl_report()
@@ -212,7 +388,7 @@ def main():
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     rccl_log, caller_debug = None, os.environ.get("NCCL_DEBUG")
     caller_nccl = {k: os.environ.get(k) for k in ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE")}
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "NCCL_DEBUG_FILE" not in os.environ:
+    if world > 1 and "NCCL_DEBUG_FILE" not in os.environ:
         rccl_log = f"/tmp/mvg_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log"
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=rccl_log)
     import torch
@@ -220,10 +396,6 @@ def main():
 
     from matvec_mpi_multiplier_amd import multiplier as mm
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    n = args.gpus
     if world != n:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run")
     # MVG_SAME_DEVICE=1 (rehearsal on a one-GPU machine): every rank on GPU 0; RCCL refuses two
@@ -241,12 +413,15 @@ def main():
     distributed = world > 1 or os.environ.get("MVG_BENCH_FORCE_DIST") == "1"
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    budget.distributed, budget.device = distributed, f"cuda:{local}"
 
     def barrier():
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
 
+    budget.current = "headline"
+    t_head = time.perf_counter()
     R = args.rows if args.rows is not None else SHARD * n
     C = args.cols
     comm = mm.Comm.from_process_group(local) if distributed else mm.Comm.init_all([local])
@@ -261,14 +436,16 @@ def main():
 
     eng.kernel_timing(args.event_every)
     gc.disable()  # no collector pause inside the timed region (K = 20 steps are 6 ms)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.multiply()
-    eng.sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    gc.enable()
+    try:
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.multiply()
+        eng.sync()
+        barrier()
+        elapsed = time.perf_counter() - t0
+    finally:
+        gc.enable()
     kt = eng.kernel_ms()
     eng.kernel_timing(0)
 
@@ -294,88 +471,11 @@ def main():
     y = eng.collect()
     if rank == 0:
         expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, "y out of range")
-
-    # ---- the same workload in bit-exact mode (the reference's sequential sums, bit for bit)
-    # The sections after the headline are reported beside it. Their parity checks never raise
-    # (expect(): recorded, exit code 1 at the end). Any other error — the environment's: out of
-    # memory, a missing reference binary — is recorded in the section's place in one process (no
-    # other rank waiting in a collective) and ends the run with N > 1 ranks, as it must.
-    def guarded(fn, *a):
-        if distributed:
-            return fn(*a)
-        try:
-            return fn(*a)
-        except Exception as exc:
-            import traceback
-
-            traceback.print_exc()
-            return {"failed": f"{type(exc).__name__}: {str(exc)[:300]}"}
-
-    exact = None
-    y_exact = None
-    if not args.no_exact:
-        got = guarded(exact_section, args, eng, n, rank, local, distributed, barrier, per_gpu, total_bytes, y)
-        exact, y_exact = got if isinstance(got, tuple) else (got, None)
-
-    # ---- several x per pass over A, rank 0 at N = 1
-    multi = None
-    if rank == 0 and n == 1 and not args.no_multi:
-        multi = guarded(multi_vector_section, local)
-
-    # ---- the text loader on config 2's input file, rank 0 at N = 1
-    loader = None
-    if rank == 0 and n == 1 and not args.no_loader:
-        loader = guarded(loader_section, R, C)
-
-    # ---- end-to-end: root's host A -> shards -> multiply -> y on the root
-    e2e = None
-    if not args.no_e2e and args.e2e_iters > 0:
-        e2e = guarded(end_to_end, args, eng, mm, R, C, rank, distributed, barrier, y, total_bytes, local)
-
-    # ---- BASELINE configs 3-5 at their own sizes on these N GPUs (the main engine's HBM is
-    # released first: config 4 is 128 GiB per GPU at N = 1)
-    configs = None
-    if not args.no_configs:
-        eng.destroy()
-        configs = guarded(baseline_configs, args, mm, comm, n, rank, local, distributed, barrier)
-
-    # ---- CPU baseline: rank 0 at N = 1 only
-    cpu = None
-    if rank == 0 and n == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.alg, R, C, y, y_exact,
-                           sweep_ps=tuple(int(p) for p in args.cpu_sweep.split(",") if p.strip()))
-        same_port, same_ref = cpu.pop("exact_vs_port", None), cpu.pop("exact_vs_reference", None)
-        if exact is not None:
-            # rowwise: the exact y against the oracle port's y (full matrix) and against the real
-            # reference's own y (its sample rows), bit for bit
-            exact["bit_identical_to_port"] = same_port
-            exact["bit_identical_to_reference_sample"] = same_ref
-
-    rccl = rccl_report(rccl_log, distributed, rank) if distributed else None
-    if rccl is not None:
-        rccl["caller_NCCL_DEBUG"] = caller_debug
-    ref_rows = None
-    if rank == 0 and args.alg == "rowwise" and C == SHARD and R >= SHARD:
-        # the weak-scaled matrix's first 16384 rows are config 2's matrix (global index i*C + j),
-        # and a row's sum does not depend on P: config 2's reference rows check every N
-        ref_rows = reference_rows_check("config 2", "rowwise", R, C, n, y, y_exact)
-
-    if rank == 0:
         pmc = pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)) or {}
-        out = {
-            "metric": "fp64 GEMV achieved HBM GB/s per GPU + end-to-end time at 1/2/4/8 MI355X",
+        report.update({
             "value": round(value, 1),
-            "unit": "GB/s",
-            "n_gpus": n,
-            "steps": args.steps,
-            "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "gflops": round(2 * R * C * args.steps / elapsed / 1e9, 1),  # whole job, 2 flops per element of A
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text inputs)",
             "config": {
                 "workload": ("config 2 weak-scaled: " if (args.rows, args.cols) == (None, SHARD) else "")
                             + f"{args.alg} of a ({R} x {C}) fp64 matrix, "
@@ -400,31 +500,164 @@ def main():
                 "bytes_per_launch": per_gpu,
                 "pmc": pmc or None,
             },
-            "cpu_baseline": cpu,
-            "reference_rows": ref_rows,
-            "rccl": rccl,
-            "exact": exact,
-            "multi_vector": multi,
-            "loader": loader,
-            "end_to_end": e2e,
-            "configs": configs,
-            "single_process": None,
-        }
+        })
+    budget.sections["setup_and_headline"] = round(time.perf_counter() - T_START, 2)
+    budget.sections["headline"] = round(time.perf_counter() - t_head, 2)
+    budget.current = None
+
+    # ---- the sections after the headline, each within the budget (Budget.run). Their parity
+    # checks never raise (expect(): recorded, exit code 1 at the end). Any other error — the
+    # environment's: out of memory, a missing reference binary — is recorded in the section's
+    # place in one process (no other rank waiting in a collective) and ends the run with N > 1
+    # ranks, as it must.
+    def guarded(fn, *a):
+        if distributed:
+            return fn(*a)
+        try:
+            return fn(*a)
+        except Exception as exc:
+            import traceback
+
+            traceback.print_exc()
+            WARNINGS.append(f"{getattr(fn, '__name__', fn)}: {type(exc).__name__}: {str(exc)[:200]}")
+            return {"failed": f"{type(exc).__name__}: {str(exc)[:300]}"}
+
+    def section(name, need_s, fn, *a, collective=True):
+        return budget.run(name, need_s, guarded, fn, *a, collective=collective)
+
+    # the same workload in bit-exact mode (the reference's sequential sums, bit for bit)
+    y_exact = None
+    if not args.no_exact:
+        got = section("exact", est_exact(per_gpu, args.steps), exact_section, args, eng, n, rank, local,
+                      distributed, barrier, per_gpu, total_bytes, y)
+        exact, y_exact = got if isinstance(got, tuple) else (got, None)
+        if rank == 0:
+            report["exact"] = exact
+
+    # CPU baseline: rank 0 at N = 1 only (the reference's own executable beside its port)
+    if rank == 0 and n == 1 and not args.no_cpu_baseline:
+        big = big_sample_rows(args, args.alg, R, C)
+        cpu = section("cpu_baseline", est_cpu_baseline(args, R, C, big_rows=big), cpu_baseline, args, args.alg, R, C,
+                      y, y_exact, None, None, None, ("spread", "compact"),
+                      tuple(int(p) for p in args.cpu_sweep.split(",") if p.strip()), big, collective=False)
+        same_port = cpu.pop("exact_vs_port", None) if isinstance(cpu, dict) else None
+        same_ref = cpu.pop("exact_vs_reference", None) if isinstance(cpu, dict) else None
+        report["cpu_baseline"] = cpu
+        with report.lock:
+            ex = report.out.get("exact")
+            if isinstance(ex, dict) and "value" in ex:
+                # rowwise: the exact y against the oracle port's y (full matrix) and against the
+                # real reference's own y (its sample rows), bit for bit
+                ex["bit_identical_to_port"] = same_port
+                ex["bit_identical_to_reference_sample"] = same_ref
+
+    # end-to-end: root's host A -> shards -> multiply -> y on the root
+    if not args.no_e2e and args.e2e_iters > 0:
+        e2e = section("end_to_end", est_e2e(total_bytes, n, args.e2e_iters, distributed), end_to_end, args, eng, mm,
+                      R, C, rank, distributed, barrier, y, total_bytes, local)
+        if rank == 0:
+            report["end_to_end"] = e2e
+
+    # BASELINE configs 3-5 at their own sizes on these N GPUs (the main engine's HBM is released
+    # first: config 4 is 128 GiB per GPU at N = 1); each config checks the budget itself
+    if not args.no_configs:
+        eng.destroy()
+        if rank == 0:
+            report["configs"] = []
+        baseline_configs(args, mm, comm, n, rank, local, distributed, barrier, budget, report, guarded)
+
+    # several x per pass over A, rank 0 at N = 1
+    if rank == 0 and n == 1 and not args.no_multi:
+        report["multi_vector"] = section("multi_vector", 8.0, multi_vector_section, local, collective=False)
+
+    # the text loader on config 2's input file, rank 0 at N = 1
+    if rank == 0 and n == 1 and not args.no_loader:
+        report["loader"] = section("loader", est_loader(R, C), loader_section, R, C, collective=False)
+
+    budget.current = "teardown"
+    rccl = rccl_report(rccl_log, distributed, rank) if distributed else None
+    if rccl is not None:
+        rccl["caller_NCCL_DEBUG"] = caller_debug
+    if rank == 0:
+        report["rccl"] = rccl
+        if args.alg == "rowwise" and C == SHARD and R >= SHARD:
+            # the weak-scaled matrix's first 16384 rows are config 2's matrix (global index i*C + j),
+            # and a row's sum does not depend on P: config 2's reference rows check every N
+            report["reference_rows"] = reference_rows_check("config 2", "rowwise", R, C, n, y, y_exact)
 
     eng.destroy()
     comm.destroy()
     if distributed:
         dist.destroy_process_group()
+    budget.current = None
     if rank == 0:
         if n > 1:
             # the executables' one-process-drives-N-GPUs path (ncclCommInitAll, grouped exchange),
             # which the rank-per-GPU sections above never run; the other ranks have exited
-            out["single_process"] = single_process_section(args, n, R, C, caller_nccl)
-        out["failures"] = FAILURES or None
-        json_out.write(json.dumps(out) + "\n")
-        json_out.flush()
+            sp = budget.run("single_process", est_single_process(R, C, n), single_process_section, args, n, R, C,
+                            caller_nccl, None, budget, collective=False)
+            report["single_process"] = sp
+            if isinstance(sp, dict) and sp.get("error"):
+                WARNINGS.append(f"single_process: the MVG_NGPUS={n} executable failed (rc {sp.get('rc')}): "
+                                f"{sp['error'][-200:]}")
+        else:
+            report["single_process"] = None
+        report.write()
     if FAILURES:
         sys.exit(1)
+
+
+# ---- section time estimates (s) for the budget: generous upper bounds from the round-4/5 box
+# records (sections_s of profiles/r05 bench lines); a section runs only if its estimate fits
+GEN_GBPS = 6.0     # host synthetic fill + first touch (16 threads)
+PIN_GBPS = 15.0    # hipHostRegister of a host matrix
+H2D_GBPS = 40.0    # per-GPU host -> device distribution (56 measured: 0.7 of it)
+REF_TEXT_GBPS = 0.08  # the reference's fscanf load of its text input, per byte of A (with the file write)
+
+
+def est_exact(per_gpu, steps):
+    return 4.0 + 3 * per_gpu / 6e12 * (2 * steps + 100)
+
+
+def est_e2e(total_bytes, n, iters, distributed):
+    gen = total_bytes / (GEN_GBPS * 1e9)
+    pin = total_bytes / (PIN_GBPS * 1e9)
+    per_iter = total_bytes / n / (H2D_GBPS * 1e9) + 0.05
+    root_send = iters * total_bytes / (H2D_GBPS * 1e9) if distributed else 0.0
+    return 4.0 + gen + pin + iters * per_iter + root_send
+
+
+def est_config(per_gpu, steps):
+    # engine create (memset + warm-up), fill, warm-up, tree + exact steps, y copies
+    return 6.0 + per_gpu / 2e10 + 2 * per_gpu / 6e12 * (steps + 40)
+
+
+def est_ref_run(nbytes, P):
+    # one run of the reference's executable on an nbytes sample: its text input written and read
+    # (fscanf), then its 100-iteration loop (~2.9 GB/s at P = 1, ~4-5 at P = 16 on the EPYC box)
+    rate = 2.5e9 if P == 1 else 3.5e9
+    return 3.0 + nbytes / (REF_TEXT_GBPS * 1e9) / 10 + 100 * nbytes / rate
+
+
+def est_cpu_baseline(args, R, C, ref_rows=None, big_rows=None, sweep=True, port_bytes=None):
+    port_bytes = min(8 * R * C, args.cpu_sample_bytes if port_bytes is None else port_bytes)
+    t = 3.0 + port_bytes / (GEN_GBPS * 1e9) + 2 * args.cpu_seconds
+    small = 8 * min(R, ref_rows or args.ref_rows) * C
+    t += 2 * est_ref_run(small, 16)
+    if sweep:
+        t += sum(est_ref_run(small, p) for p in (1, 2, 4, 8))
+    if big_rows:
+        big = 8 * min(R, big_rows) * C
+        t += est_ref_run(big, 16) + est_ref_run(big, 1)
+    return t
+
+
+def est_loader(R, C):
+    return 5.0 + 7 * R * C / 0.8e9 + 2 * 8 * R * C / (GEN_GBPS * 1e9)
+
+
+def est_single_process(R, C, n):
+    return 30.0 + 60 * 8 * R * C / n / 7e12 + 8 * R * C / 20e9
 
 
 def warm(e, min_launches, distributed, local, seconds=0.1):
@@ -451,14 +684,16 @@ def warm(e, min_launches, distributed, local, seconds=0.1):
     e.sync()
 
 
-def single_process_section(args, n, R, C, caller_nccl=None, exe=None):
+def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=None):
     """The drop-in executables' single-process form of the same workload: ONE process drives all
     N GPUs (mvg_comm_init_all -> ncclCommInitAll over N devices, the grouped ncclCommSplit and the
     exchange grouped over the local devices, csrc/engine.cpp), which the one-rank-per-GPU
     sections above never run. Rank 0 starts `MVG_NGPUS=N MVG_SYNTH=device bin/multiplier_<alg>
     R C` as a child process once the process group is gone, and records its device-resident line
     and its y against config 2's reference rows. A failure is recorded here, never fatal; the
-    reference's own grid and gather: multiplier_blockwise.c:299-306, :144-210."""
+    reference's own grid and gather: multiplier_blockwise.c:299-306, :144-210. The child's time
+    limit is what is left of the budget (at most 300 s); a failed run is also a top-level
+    warning of the line (main)."""
     import re
     import shutil
     import subprocess
@@ -487,7 +722,8 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None):
         env.update(MVG_NGPUS=str(n), MVG_SYNTH="device", MVG_ITERS=str(iters), MVG_Y_OUT=ypath)
         cmd = [exe, str(R), str(C)]
         t0 = time.perf_counter()
-        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=300)
+        limit = 300.0 if budget is None else max(10.0, min(300.0, budget.left() - 5.0))
+        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=limit)
         wall = time.perf_counter() - t0
         out = {"ran": True, "command": f"MVG_NGPUS={n} MVG_SYNTH=device MVG_ITERS={iters} "
                                       f"bin/multiplier_{args.alg} {R} {C}", "rc": r.returncode,
@@ -712,19 +948,25 @@ BASELINE_CONFIGS = [
 ]
 
 
-def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
+def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier, budget=None, report=None, guarded=None):
     """Configs 3-5 of BASELINE.json on the same N GPUs: device-resident synthetic inputs, one step
     = GEMV on every shard + the algorithm's RCCL exchange (col: ncclReduce of R doubles; block:
     row-communicator ncclReduce + leaders' ncclGather on the utils.c:26-37 grid, 2 x 4 at N = 8;
     row: ncclGather), --config-steps steps timed between barriers, max over ranks. A config
     whose shard does not fit in free HBM on every rank is skipped on all of them (the decision
-    is all-reduced so no rank waits in a collective another skipped)."""
+    is all-reduced so no rank waits in a collective another skipped), as is one whose estimate
+    no longer fits in the budget. Each finished config goes straight into `report` (rank 0), so
+    a truncated line keeps it."""
     import torch
     import torch.distributed as dist
 
+    budget = budget or Budget(float("inf"), distributed, f"cuda:{local}")
+    guarded = guarded or (lambda fn, *a: fn(*a))
     out = []
     by_num = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}
-    for name, alg, R, C in (by_num[int(k)] for k in args.configs.split(",") if k.strip()):
+    e2e_set = {int(k) for k in args.config_e2e.split(",") if k.strip()}
+    for k in (int(k) for k in args.configs.split(",") if k.strip()):
+        name, alg, R, C = by_num[k]
         sh = mm.plan_shard(alg, R, C, n, rank)
         part = R if alg == "colwise" else sh.y_len
         need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + (9 + n) * part + R) + (1 << 30)  # + exact-mode gather buffer
@@ -733,96 +975,160 @@ def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier):
         if distributed:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if float(ok[0]) < 1.0:
-            out.append({"config": name, "alg": alg, "R": R, "C": C, "skipped": f"needs {need >> 30} GiB of HBM per GPU"})
-            continue
-        def timed(e, steps):
-            e.kernel_timing(args.event_every)
-            barrier()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                e.multiply()
-            e.sync()
-            barrier()
-            el = time.perf_counter() - t0
-            kt = e.kernel_ms()
-            e.kernel_timing(0)
-            by_rank[0] = per_rank(kt.avg_ms, distributed, local)
-            t = torch.tensor([el, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
-            if distributed:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return float(t[0]), float(t[1])
-
-        by_rank = [None]
-
-        total = sum(8 * (s.n_rows * s.n_cols + s.n_cols + (R if alg == "colwise" else s.y_len))
-                    for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
-        per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
-        exact = None
-        e = mm.Multiplier(alg, R, C, comm)
-        try:
-            e.fill_synth()
-            warm(e, 3, distributed, local)
-            el, kms = timed(e, args.config_steps)
-            tree_by_rank = by_rank[0]
-            y = e.collect()
-            yx = None
-            if rank == 0:
-                expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range")
-            e2e = None
-            if not args.no_e2e and args.e2e_iters > 0 and 8 * R * C <= args.config_e2e_bytes:
-                # north_star's end-to-end time on the tall-skinny config too: the root's host A
-                # distributed over every GPU's link, multiplied, y on the root (same values as the
-                # device-resident fill, so the exact section below still multiplies the same A)
-                e2e = end_to_end(args, e, mm, R, C, rank, distributed, barrier, y, total, local)
-            if not args.no_exact:
-                # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
-                # every partial to rank 0, the reference's combine order there)
-                e.set_exact(True)
-                warm(e, 2, distributed, local)
-                xsteps = max(5, args.config_steps // 2)
-                xel, xkms = timed(e, xsteps)
-                yx = e.collect()
-                xkernel = exact_kernel_name(e)
-                e.set_exact(False)
-                exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
-                         "gflops": round(2 * R * C * xsteps / xel / 1e9, 1),
-                         "steps": xsteps, "kernel": xkernel, "kernel_ms": round(xkms, 5),
-                         "kernel_ms_by_rank": by_rank[0], "pmc": pmc_summary(sh.n_rows, sh.n_cols, xkernel),
-                         "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
-                if rank == 0:
-                    rel = float(np.max(np.abs(yx - y) / np.abs(y)))
-                    expect(rel <= 1e-12, f"{name}: exact y differs from the tree-summed y by {rel}")
-                    exact["max_rel_vs_tree"] = rel
-        finally:
-            e.destroy()
-        gr, gc = mm.get_2_most_closest_multipliers(n)
-        entry = {
-            "config": name, "alg": alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
-            "grid": [gr, gc] if alg == "blockwise" else None,
-            "value": round(total * args.config_steps / el / 1e9, 1), "unit": "GB/s",
-            "ms_per_step": round(el / args.config_steps * 1e3, 4), "steps": args.config_steps,
-            "gflops": round(2 * R * C * args.config_steps / el / 1e9, 1),
-            "kernel": kernel_name(sh), "kernel_ms": round(kms, 5), "kernel_ms_by_rank": tree_by_rank,
-            "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
-            "pmc": pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)),
-            "exact": exact,
-            "end_to_end": e2e,
-        }
-        if rank == 0:
-            entry["reference_rows"] = reference_rows_check(name, alg, R, C, n, y, yx)
-            if n == 1 and not args.no_cpu_baseline and not args.no_config_cpu_baseline:
-                # the reference on a leading-row slice at the host's core count, and the -O2 port
-                # on the whole config where host memory allows (config 4: its leading rows)
-                try:
-                    ref_rows = min(R, max(128, int(args.config_ref_bytes // (8 * C))))
-                    entry["cpu_baseline"] = cpu_baseline(args, alg, R, C, y, None, ref_rows=ref_rows,
-                                                         sample_bytes=args.config_cpu_sample_bytes,
-                                                         cpu_seconds=args.config_cpu_seconds, placements=("spread",))
-                except Exception as exc:  # the baseline must never sink the bench
-                    entry["cpu_baseline"] = f"failed: {str(exc)[:300]}"
+            entry = {"config": name, "alg": alg, "R": R, "C": C, "skipped": f"needs {need >> 30} GiB of HBM per GPU"}
+        else:
+            per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
+            entry = budget.run(name, est_config(per, args.config_steps), guarded, one_config, args, mm, comm, n, rank,
+                               local, distributed, barrier, budget, guarded, name, alg, R, C, k in e2e_set)
+            if not isinstance(entry, dict) or "value" not in entry:
+                entry = {"config": name, "alg": alg, "R": R, "C": C, **(entry if isinstance(entry, dict) else {})}
         out.append(entry)
-        del y, yx
+        if report is not None and rank == 0:
+            report.append("configs", entry)
     return out
+
+
+def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, guarded, name, alg, R, C, with_e2e):
+    """One BASELINE config on the N GPUs (baseline_configs): tree-mode steps, then — within the
+    budget and where host memory holds its A — the end-to-end loop, then the bit-exact steps; on
+    rank 0 its y against the reference's own rows and, at N = 1, its CPU baseline."""
+    import torch
+    import torch.distributed as dist
+
+    sh = mm.plan_shard(alg, R, C, n, rank)
+    part = R if alg == "colwise" else sh.y_len
+
+    def timed(e, steps):
+        e.kernel_timing(args.event_every)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            e.multiply()
+        e.sync()
+        barrier()
+        el = time.perf_counter() - t0
+        kt = e.kernel_ms()
+        e.kernel_timing(0)
+        by_rank[0] = per_rank(kt.avg_ms, distributed, local)
+        t = torch.tensor([el, kt.avg_ms], dtype=torch.float64, device=f"cuda:{local}")
+        if distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0]), float(t[1])
+
+    by_rank = [None]
+    total = sum(8 * (s.n_rows * s.n_cols + s.n_cols + (R if alg == "colwise" else s.y_len))
+                for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
+    per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
+    exact = None
+    e2e = None
+    e = mm.Multiplier(alg, R, C, comm)
+    try:
+        e.fill_synth()
+        warm(e, 3, distributed, local)
+        el, kms = timed(e, args.config_steps)
+        tree_by_rank = by_rank[0]
+        y = e.collect()
+        yx = None
+        if rank == 0:
+            expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range")
+        if with_e2e and not args.no_e2e and args.e2e_iters > 0:
+            # north_star's end-to-end time at every config: the root's host A distributed over
+            # every GPU's link, multiplied, y on the root (same values as the device-resident
+            # fill, so the exact steps below still multiply the same A), wherever host memory
+            # (and /dev/shm at N > 1) holds A, measured now
+            fit, mem = e2e_memory_fit(R, C, distributed, local)
+            if not fit:
+                e2e = {"skipped": "memory", **mem}
+            else:
+                e2e = budget.run(f"{name} end_to_end", est_e2e(total, n, args.e2e_iters, distributed), guarded,
+                                 end_to_end, args, e, mm, R, C, rank, distributed, barrier, y, total, local)
+                if isinstance(e2e, dict):
+                    e2e["host_memory"] = mem
+        if not args.no_exact:
+            # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
+            # every partial to rank 0, the reference's combine order there)
+            e.set_exact(True)
+            warm(e, 2, distributed, local)
+            xsteps = max(5, args.config_steps // 2)
+            xel, xkms = timed(e, xsteps)
+            yx = e.collect()
+            xkernel = exact_kernel_name(e)
+            e.set_exact(False)
+            exact = {"value": round(total * xsteps / xel / 1e9, 1), "ms_per_step": round(xel / xsteps * 1e3, 4),
+                     "gflops": round(2 * R * C * xsteps / xel / 1e9, 1),
+                     "steps": xsteps, "kernel": xkernel, "kernel_ms": round(xkms, 5),
+                     "kernel_ms_by_rank": by_rank[0], "pmc": pmc_summary(sh.n_rows, sh.n_cols, xkernel),
+                     "kernel_frac": round(per / (xkms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if xkms > 0 else None}
+            if rank == 0:
+                rel = float(np.max(np.abs(yx - y) / np.abs(y)))
+                expect(rel <= 1e-12, f"{name}: exact y differs from the tree-summed y by {rel}")
+                exact["max_rel_vs_tree"] = rel
+    finally:
+        e.destroy()
+    gr, gcols = mm.get_2_most_closest_multipliers(n)
+    entry = {
+        "config": name, "alg": alg, "R": R, "C": C, "shard": [sh.n_rows, sh.n_cols],
+        "grid": [gr, gcols] if alg == "blockwise" else None,
+        "value": round(total * args.config_steps / el / 1e9, 1), "unit": "GB/s",
+        "ms_per_step": round(el / args.config_steps * 1e3, 4), "steps": args.config_steps,
+        "gflops": round(2 * R * C * args.config_steps / el / 1e9, 1),
+        "kernel": kernel_name(sh), "kernel_ms": round(kms, 5), "kernel_ms_by_rank": tree_by_rank,
+        "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
+        "pmc": pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)),
+        "exact": exact,
+        "end_to_end": e2e if with_e2e else "not requested (--config-e2e)",
+    }
+    if rank == 0:
+        entry["reference_rows"] = reference_rows_check(name, alg, R, C, n, y, yx)
+        if n == 1 and not args.no_cpu_baseline and not args.no_config_cpu_baseline:
+            # the reference on a leading-row slice at the host's core count, and the -O2 port on
+            # the whole config where host memory allows (config 4: its leading rows)
+            ref_rows = min(R, max(128, int(args.config_ref_bytes // (8 * C))))
+            entry["cpu_baseline"] = budget.run(
+                f"{name} cpu_baseline",
+                est_cpu_baseline(args, R, C, ref_rows=ref_rows, sweep=False, port_bytes=args.config_cpu_sample_bytes),
+                guarded, cpu_baseline, args, alg, R, C, y, None, ref_rows, args.config_cpu_sample_bytes,
+                args.config_cpu_seconds, ("spread",), (), None, collective=False)
+    return entry
+
+
+def host_mem_free() -> int:
+    """Host bytes this process may still take: MemAvailable, capped by its cgroup's memory.max
+    less memory.current when a limit is set (the GPU pool's per-command cap)."""
+    free = None
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                free = int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    try:
+        lim = open("/sys/fs/cgroup/memory.max").read().strip()
+        if lim != "max":
+            cap = int(lim) - int(open("/sys/fs/cgroup/memory.current").read().strip())
+            free = cap if free is None else min(free, cap)
+    except (OSError, ValueError):
+        pass
+    return max(0, free or 0)
+
+
+def e2e_memory_fit(R, C, distributed, local, margin=8 << 30):
+    """Whether the end-to-end loop's host copy of A (R x C fp64; in /dev/shm at N > 1, a
+    process's own memory at N = 1) fits with `margin` and 5 % to spare, on every rank (MIN)."""
+    import torch
+    import torch.distributed as dist
+
+    from matvec_mpi_multiplier_amd.hostshare import shm_free_bytes
+
+    need = 8 * R * C
+    free = host_mem_free()
+    shm = shm_free_bytes() if distributed else None
+    ok = free >= need * 1.05 + margin and (shm is None or shm >= need + (1 << 30))
+    if distributed:
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = float(t[0]) >= 1.0
+    return ok, {"need_bytes": need, "host_free_bytes": free, "shm_free_bytes": shm}
 
 
 SLICES = os.path.join(REPO, "tests", "golden", "config_slices.npz")
@@ -989,7 +1295,19 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
     have_shared = A is not None
     if distributed and not have_shared and rank == 0:
         A = mm.synth_host(R, C, 42)  # root-only copy for the root_send distribution
-    pinned = A is not None and _l.mvg_host_register(A.ctypes.data, A.nbytes) == 0
+    # page-lock what this rank's GPU reads: all of A on the root (it also stages every peer's shard
+    # for root_send) and at N = 1; a peer's own rows otherwise (its row block's lines; the column
+    # split's strip spans every row)
+    reg = None
+    if A is not None:
+        sh = eng.shard(0)
+        if distributed and rank != 0 and eng.name != "colwise":
+            reg = host_rows_region(A, sh.row_off, sh.row_off + sh.n_rows)
+        else:
+            reg = (A.ctypes.data, A.nbytes)
+        if _l.mvg_host_register(*reg) != 0:
+            reg = None
+    pinned = reg is not None
     if have_shared:
         out["shared"] = timed(lambda: (eng.distribute_shared(A, x), eng.multiply(), eng.collect())[2])
         out["shared"]["distribution"] = ("per-GPU H2D from " + ("shared " if distributed else "")
@@ -999,7 +1317,7 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
                                           eng.collect())[2])
         out["root_send"]["distribution"] = "root H2D staging + ncclSend over xGMI"
     if pinned:
-        _l.mvg_host_unregister(A.ctypes.data)
+        _l.mvg_host_unregister(reg[0])
     if shared is not None:
         eng._keep = None
         del A
@@ -1017,6 +1335,16 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
             link["frac_of_copy"] = round(per_gpu / link["h2d_copy_GBps"], 4)
         out["roofline"] = link
     return out
+
+
+def host_rows_region(A, r0, r1, page=4096):
+    """(address, bytes) of rows [r0, r1) of the row-major host matrix A, widened to whole pages
+    within A's buffer (page-locking works on pages)."""
+    row = A.shape[1] * A.itemsize
+    base, end = A.ctypes.data, A.ctypes.data + A.nbytes
+    lo = max(base, (base + r0 * row) // page * page)
+    hi = min(end, -(-(base + r1 * row) // page) * page)
+    return lo, max(0, hi - lo)
 
 
 def n_ranks(distributed):
@@ -1068,36 +1396,33 @@ def pcie_roofline(local):
 
 
 def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_bytes=None, cpu_seconds=None,
-                 placements=("spread", "compact"), sweep_ps=()):
+                 placements=("spread", "compact"), sweep_ps=(), big_rows=None):
     """The reference's CPU path timed on this host. Preferred: the real reference (oracle/_ref,
     built from its own sources, run with MPICH's mpiexec on P = the port's thread count) on the
-    leading `ref_rows` rows of the same matrix, kind "reference"; its 100-iteration loop is fixed
-    in its source. Always also: the oracle port (below), reported under "port" (or as the
-    baseline itself, kind "port", when the reference cannot run here). `sweep_ps`: the reference
-    also runs on the same sample at those rank counts (`sweep`: its time, GB/s, speed-up and
-    efficiency as its README defines them, S = T1 / TP and E = S / P, README.md:47-50)."""
+    leading rows of the same matrix, kind "reference"; its 100-iteration loop is fixed in its
+    source. Always also: the oracle port (below), reported under "port" (or as the baseline
+    itself, kind "port", when the reference cannot run here).
+
+    Two samples. The small one (`ref_rows` rows) picks the placement (the port's spread CPUs or
+    consecutive cores: the reference is communication-bound, its root scatters A through MPI
+    shared memory every iteration) and carries the rank sweep `sweep_ps` (`sweep`: time, GB/s,
+    speed-up and efficiency as its README defines them, S = T1 / TP and E = S / P,
+    README.md:47-50). With `big_rows`, the reference then runs on a sample at least twice the
+    last-level cache of the CPUs it uses (`host_cache`, from sysfs) at P and at P = 1 on the
+    winning placement, and that beyond-cache run is the baseline's `value`; the small sample's
+    figures stay under `small_sample`."""
     ref_rows = args.ref_rows if ref_rows is None else ref_rows
     port = cpu_port_baseline(args, alg, R, C, y_gpu, y_exact, sample_bytes, cpu_seconds)
     if args.no_ref_baseline:
         return port
-    from oracle import ref_runner
+    from oracle import cpuset, ref_runner
 
     P = port["cores"]
     cpus = port["placement"]["cpus"]
-    rows = min(R, ref_rows)
-    if alg in ("rowwise", "blockwise"):
-        from oracle import oracle
-
-        gr = P if alg == "rowwise" else oracle.grid_shape(P)[0]
-        rows = max(gr, rows - rows % gr)
+    rows = splittable_rows(alg, min(R, ref_rows), P)
     if not ref_runner.available(alg) or not _splits(alg, rows, C, P):
         port["reference"] = "not run: oracle/_ref or mpiexec absent, or the sample does not split"
         return port
-    # the reference is communication-bound (its root scatters A through MPI shared memory every
-    # iteration): it runs once on the port's spread placement and once on consecutive cores, and
-    # the faster run is its baseline (both recorded)
-    from oracle import cpuset
-
     runs = []
     sets = {"spread": cpus, "compact": None}
     for label in placements:
@@ -1111,23 +1436,114 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
         port["reference"] = "not run: " + "; ".join(port.get("reference_errors", []))
         return port
     label, cpus, r = min(runs, key=lambda t: t[2]["seconds"])
-    placements = {lab: round(8 * (rows * C + C + rows) / rr["seconds"] / 1e9, 3) for lab, _, rr in runs}
+    by_placement = {lab: round(8 * (rows * C + C + rows) / rr["seconds"] / 1e9, 3) for lab, _, rr in runs}
     rel = float(np.max(np.abs(y_gpu[:rows] - r["y"]) / np.abs(r["y"])))
     expect(rel <= 1e-12, f"GPU y differs from the reference's own y: {rel}")
     nbytes = 8 * (rows * C + C + rows)
     sweep = ref_sweep(args, alg, rows, C, P, r["seconds"], label, sweep_ps, nbytes) if sweep_ps else None
-    return {"value": round(nbytes / r["seconds"] / 1e9, 3), "unit": "GB/s", "cores": P, "kind": "reference",
-            "sweep": sweep,
-            "ms_per_step": round(r["seconds"] * 1e3, 3), "iters": 100,
-            "sample": f"leading {rows} of {R} rows ({rows}x{C}) {alg}: the reference's own executable "
-                      f"(oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its text inputs, its "
-                      f"100-iteration loop (distribution from the root + sequential sums + collection); "
-                      f"run {r['wall_s']:.1f} s incl. text loading; GPU y matches its y to {rel:.1e}",
-            "host_cpu": host_cpu(), "placement": {**cpuset.describe(cpus), "kind": label, "GBps_by_placement": placements},
-            "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")},
-            "exact_vs_port": port.get("exact_vs_port"),
-            **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}
-               if y_exact is not None and alg == "rowwise" else {})}
+    cache = host_cache(cpus)
+
+    def sample_text(nrows, rr, relv):
+        return (f"leading {nrows} of {R} rows ({nrows}x{C}, {8 * nrows * C / 2 ** 20:.0f} MiB) {alg}: the "
+                f"reference's own executable (oracle/_ref, MPICH mpiexec -n {P}, gcc -O0 as its test.sh) on its "
+                f"text inputs, its 100-iteration loop (distribution from the root + sequential sums + "
+                f"collection); run {rr['wall_s']:.1f} s incl. text loading; GPU y matches its y to {relv:.1e}")
+
+    small = {"value": round(nbytes / r["seconds"] / 1e9, 3), "ms_per_step": round(r["seconds"] * 1e3, 3),
+             "rows": rows, "bytes": nbytes, "sample": sample_text(rows, r, rel)}
+    out = {"value": small["value"], "unit": "GB/s", "cores": P, "kind": "reference", "sweep": sweep,
+           "ms_per_step": small["ms_per_step"], "iters": 100, "sample": small["sample"],
+           "host_cpu": host_cpu(), "host_cache": cache,
+           "placement": {**cpuset.describe(cpus), "kind": label, "GBps_by_placement": by_placement},
+           "port": {k: port[k] for k in ("value", "ms_per_step", "cores", "sample")},
+           "exact_vs_port": port.get("exact_vs_port"),
+           **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}
+              if y_exact is not None and alg == "rowwise" else {})}
+    l3 = (cache or {}).get("l3_bytes")
+    out["sample_over_l3"] = round(nbytes / l3, 2) if l3 else None
+    if big_rows:
+        brows = splittable_rows(alg, min(R, big_rows), P)
+        if brows <= rows:
+            out["big_sample"] = f"not run: {brows} rows is not beyond the small sample"
+        else:
+            bbytes = 8 * (brows * C + C + brows)
+            try:
+                rb = ref_runner.run(alg, brows, C, P, timeout=args.ref_timeout, cpus=cpus, rows=np.arange(brows))
+                relb = float(np.max(np.abs(y_gpu[:brows] - rb["y"]) / np.abs(rb["y"])))
+                expect(relb <= 1e-12, f"GPU y differs from the reference's own y (beyond-cache sample): {relb}")
+                pts = [{"P": P, "s_per_iter": round(rb["seconds"], 6), "GBps": round(bbytes / rb["seconds"] / 1e9, 3)}]
+                if P > 1 and 1 in sweep_ps:
+                    try:
+                        r1 = ref_runner.run(alg, brows, C, 1, timeout=args.ref_timeout,
+                                            cpus=cpuset.pick(1, gpu_numa_node()), rows=np.arange(brows))
+                        pts.insert(0, {"P": 1, "s_per_iter": round(r1["seconds"], 6),
+                                       "GBps": round(bbytes / r1["seconds"] / 1e9, 3)})
+                    except Exception as exc:  # a sweep point must never sink the bench
+                        out["big_sample_errors"] = [f"P=1: {str(exc)[:160]}"]
+                t1 = pts[0]["s_per_iter"] if pts[0]["P"] == 1 else None
+                for pt in pts:
+                    pt["speedup"] = round(t1 / pt["s_per_iter"], 3) if t1 else None
+                    pt["efficiency"] = round(t1 / pt["s_per_iter"] / pt["P"], 3) if t1 else None
+                out.update(value=round(bbytes / rb["seconds"] / 1e9, 3), ms_per_step=round(rb["seconds"] * 1e3, 3),
+                           sample=sample_text(brows, rb, relb), sample_over_l3=round(bbytes / l3, 2) if l3 else None,
+                           sweep_beyond_cache={"points": pts, "semantics": "the same executable on the beyond-cache "
+                                               "sample; S = T1/TP, E = S/P (README.md:47-50)"},
+                           small_sample=small)
+                if y_exact is not None and alg == "rowwise":
+                    out["exact_vs_reference"] = bool(np.array_equal(y_exact[:brows], rb["y"]))
+            except Exception as exc:  # the small sample's figures stand
+                out["big_sample"] = f"failed: {str(exc)[:300]}"
+    return out
+
+
+def splittable_rows(alg, rows, P):
+    """`rows` rounded down to what the algorithm splits over P ranks (a multiple of the ranks
+    over rows: P for the row split, the grid's rows for the block split)."""
+    if alg in ("rowwise", "blockwise"):
+        from oracle import oracle
+
+        gr = P if alg == "rowwise" else oracle.grid_shape(P)[0]
+        rows = max(gr, rows - rows % gr)
+    return rows
+
+
+def big_sample_rows(args, alg, R, C, factor=2.0, min_bytes=1 << 30):
+    """Rows of the beyond-cache CPU sample: at least `factor` x the host's last-level cache
+    (all of it, every instance: the reference's ranks may run anywhere in the quota) and at least
+    1 GiB of A, at most the whole matrix."""
+    cache = host_cache(None) or {}
+    need = max(min_bytes, factor * (cache.get("l3_bytes_system") or 0))
+    return int(min(R, -(-int(need) // (8 * C))))
+
+
+def host_cache(cpus=None):
+    """The last-level (L3) cache from sysfs for the CPUs `cpus` (default: every CPU of the host):
+    size of one instance, the distinct instances those CPUs use, and their total (`l3_bytes`);
+    `l3_bytes_system`: all instances on the host. None when sysfs has no L3."""
+    base = "/sys/devices/system/cpu"
+
+    def size_bytes(txt):
+        txt = txt.strip()
+        mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(txt[-1:], 1)
+        return int(txt.rstrip("KMG")) * mult
+
+    try:
+        inst = {}
+        for path in glob.glob(f"{base}/cpu[0-9]*/cache/index*/level"):
+            if open(path).read().strip() != "3":
+                continue
+            d = os.path.dirname(path)
+            cpu = int(d.split("/cpu")[-1].split("/")[0])
+            shared = open(f"{d}/shared_cpu_list").read().strip()
+            inst.setdefault(shared, [size_bytes(open(f"{d}/size").read()), set()])[1].add(cpu)
+        if not inst:
+            return None
+        used = [v for v in inst.values() if cpus is None or v[1] & set(cpus)]
+        return {"l3_instance_bytes": max(v[0] for v in inst.values()), "l3_instances": len(used),
+                "l3_bytes": sum(v[0] for v in used), "l3_bytes_system": sum(v[0] for v in inst.values()),
+                "source": f"{base}/cpu*/cache/index*/ (level 3)"}
+    except (OSError, ValueError):
+        return None
 
 
 def ref_sweep(args, alg, rows, C, P, seconds_at_P, label_at_P, ps, nbytes):

@@ -108,6 +108,29 @@ typedef struct mvg_xstep {
 int mvg_plan_exchange(int alg, int64_t R, int64_t C, int nranks, int rank, int force_collect,
                       mvg_xstep* steps, int max_steps, int* nsteps);
 
+/* Test hook: the calls one process driving `ndev` devices issues (the executables'
+ * MVG_NGPUS=G form: ncclCommSplit of the schedule's sub-communicators, then one multiply's
+ * exchange), produced by the engine's own exchange code with a recorder in place of RCCL, so no
+ * device is needed. `exact` != 0: exact mode's exchange (rank-order gather to rank 0 + the
+ * combine kernel there). Calls are listed in issue order; `group` numbers the
+ * ncclGroupStart/End bracket each was issued in (-1: outside any, the combine kernel); `comm`
+ * is -1 for the world communicator, else the group whose split created it;
+ * color -1 = NCCL_SPLIT_NOCOLOR; src/dst are MVG_X_BUF_*
+ * (MVG_X_BUF_GATHERED: rank 0's gather buffer in exact mode), -1 where the call has none.
+ * Reference interface it stands for: multiplier_blockwise.c:144-210 (gather_local_results),
+ * multiplier_colwise.c:124, multiplier_rowwise.c:141. */
+#define MVG_XCALL_SPLIT   0
+#define MVG_XCALL_GATHER  1
+#define MVG_XCALL_REDUCE  2
+#define MVG_XCALL_COMBINE 3
+#define MVG_X_BUF_GATHERED 3
+typedef struct mvg_xcall {
+    int     group, kind, rank, comm, color, key, root, src, dst;
+    int64_t count;
+} mvg_xcall;
+int mvg_debug_trace_exchange(int alg, int64_t R, int64_t C, int ndev, int exact, mvg_xcall* calls, int max_calls,
+                             int* ncalls);
+
 /* ------------------------------------------------------------------ synthetic inputs
  * value(seed, idx) = (double)k / 10000.0, k = floor(splitmix64(s0 + idx*gamma) * 10000 / 2^64),
  * s0 = splitmix64(seed), gamma = 0x9E3779B97F4A7C15. Every value is exactly what "%.4f" text
@@ -205,6 +228,13 @@ int mvg_gemv_exact_variant(const double* d_A, int64_t lda, const double* d_x, do
 int mvg_gemv_exact_variant_count(void);
 int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k);
 const char* mvg_gemv_exact_variant_name(int variant);
+/* Test hooks of the exact dispatch (no counterpart in the reference). mvg_debug_set_cu_count:
+ * the CU count the dispatch plans whole rounds of workgroups for (0 = the current device's).
+ * mvg_debug_set_exact_even_lds: the LDS reservation of the evenly placed form in bytes (0 = its
+ * own 96 KiB); above the CU's 160 KiB the runtime refuses the launch, which drives the fallback
+ * to the one-wave form (same sums); it also forgets earlier refusals. */
+int mvg_debug_set_cu_count(int n);
+int mvg_debug_set_exact_even_lds(int64_t bytes);
 
 /* The same bit-exact product over A in column panels (the engine's device layout in exact mode,
  * DESIGN §4b): panel p holds columns [p*P, p*P + P) of all m rows, row i of it at

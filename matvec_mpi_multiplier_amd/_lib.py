@@ -68,9 +68,22 @@ class XStep(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class XCall(C.Structure):
+    """mvg_xcall: one call of the single-process exchange (mvg_debug_trace_exchange)."""
+
+    _fields_ = [
+        ("group", C.c_int), ("kind", C.c_int), ("rank", C.c_int), ("comm", C.c_int), ("color", C.c_int),
+        ("key", C.c_int), ("root", C.c_int), ("src", C.c_int), ("dst", C.c_int), ("count", C.c_int64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 X_GATHER, X_REDUCE = 0, 1
 X_WORLD, X_ROW, X_COL = 0, 1, 2
-X_BUF_PART, X_BUF_ROW, X_BUF_Y = 0, 1, 2
+X_BUF_PART, X_BUF_ROW, X_BUF_Y, X_BUF_GATHERED = 0, 1, 2, 3
+XCALL_SPLIT, XCALL_GATHER, XCALL_REDUCE, XCALL_COMBINE = 0, 1, 2, 3
 MAX_XSTEPS = 4
 
 _p = C.c_void_p
@@ -115,6 +128,10 @@ SIGNATURES = {
     "mvg_gemv_exact_variant": (C.c_int, [_p, _i64, _p, _p, _i64, _i64, C.c_int, _p]),
     "mvg_gemv_exact_variant_count": (C.c_int, []),
     "mvg_gemv_exact_auto_variant": (C.c_int, [_i64, _i64, _i64]),
+    "mvg_debug_set_cu_count": (C.c_int, [C.c_int]),
+    "mvg_debug_trace_exchange": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.POINTER(XCall), C.c_int,
+                                           C.POINTER(C.c_int)]),
+    "mvg_debug_set_exact_even_lds": (C.c_int, [_i64]),
     "mvg_gemv_exact_variant_name": (C.c_char_p, [C.c_int]),
     "mvg_gemv_exact_panels": (C.c_int, [_p, _i64, _i64, _p, _p, _i64, _i64, C.c_int, _p]),
     "mvg_panel_relayout": (C.c_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p]),

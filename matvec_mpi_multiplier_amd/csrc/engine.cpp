@@ -128,6 +128,80 @@ struct mvg_engine {
 
 namespace {
 
+// The exchange's device-side calls — RCCL's communicator splits and collectives, and exact
+// mode's combine kernel on rank 0 — go through one interface: RCCL and the kernels on the
+// devices (DeviceXOps), or a recorder that lists them in issue order (TraceXOps,
+// mvg_debug_trace_exchange: the single-process G-device schedule, run on a host without GPUs).
+struct XOps {
+    virtual ~XOps() = default;
+    virtual ncclResult_t group_start() = 0;
+    virtual ncclResult_t group_end() = 0;
+    virtual void set_device(int dev) = 0;
+    virtual ncclResult_t split(ncclComm_t world, int color, int key, ncclComm_t* out) = 0;
+    virtual ncclResult_t gather(const double* src, double* dst, size_t count, int root, ncclComm_t comm,
+                                hipStream_t st) = 0;
+    virtual ncclResult_t reduce(const double* src, double* dst, size_t count, int root, ncclComm_t comm,
+                                hipStream_t st) = 0;
+    virtual int combine(const mvg_engine* e, const Shard& s, hipStream_t st) = 0;
+};
+
+struct DeviceXOps final : XOps {
+    ncclResult_t group_start() override { return ncclGroupStart(); }
+    ncclResult_t group_end() override { return ncclGroupEnd(); }
+    void set_device(int dev) override { (void)hipSetDevice(dev); }
+    ncclResult_t split(ncclComm_t world, int color, int key, ncclComm_t* out) override {
+        return ncclCommSplit(world, color, key, out, nullptr);
+    }
+    ncclResult_t gather(const double* src, double* dst, size_t count, int root, ncclComm_t comm,
+                        hipStream_t st) override {
+        return ncclGather(src, dst, count, ncclFloat64, root, comm, st);
+    }
+    ncclResult_t reduce(const double* src, double* dst, size_t count, int root, ncclComm_t comm,
+                        hipStream_t st) override {
+        return ncclReduce(src, dst, count, ncclFloat64, ncclSum, root, comm, st);
+    }
+    int combine(const mvg_engine* e, const Shard& s, hipStream_t st) override {
+        return e->alg == MVG_ALG_COLWISE ? launch_combine_mpich_reduce(s.gbuf, e->nranks, e->R, s.dy, st)
+                                         : launch_combine_grid_rows(s.gbuf, s.plan.grid_rows, s.plan.grid_cols,
+                                                                    s.plan.y_len, s.dy, st);
+    }
+};
+
+DeviceXOps g_device_ops;
+
+// A shard keeps a grid-row buffer when a step of its schedule reads or writes one.
+bool needs_row_buffer(const Shard& s) {
+    bool need = false;
+    for (int k = 0; k < s.nsteps; ++k)
+        need |= s.steps[k].member && (s.steps[k].dst == MVG_X_BUF_ROW || s.steps[k].src == MVG_X_BUF_ROW);
+    return need;
+}
+
+// Sub-communicators of the exchange schedule. ncclCommSplit is collective over the world, so
+// every local rank calls it for every split step, inside one group per step.
+int split_steps(std::vector<Shard>& shards, XOps& ops) {
+    const int nsteps = shards.empty() ? 0 : shards[0].nsteps;
+    for (int k = 0; k < nsteps; ++k) {
+        if (shards[0].steps[k].comm == MVG_X_WORLD) {
+            for (auto& s : shards) s.xcomm[k] = s.world;
+            continue;
+        }
+        ncclResult_t r = ops.group_start();
+        if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+        for (auto& s : shards) {
+            ops.set_device(s.device);
+            const mvg_xstep& st = s.steps[k];
+            r = ops.split(s.world, st.member ? st.color : NCCL_SPLIT_NOCOLOR, st.key, &s.xcomm[k]);
+            s.owns_xcomm[k] = true;
+            if (r != ncclSuccess) break;
+        }
+        const ncclResult_t r2 = ops.group_end();
+        if (r != ncclSuccess) return nccl_fail(r, "ncclCommSplit");
+        if (r2 != ncclSuccess) return nccl_fail(r2, "ncclCommSplit group");
+    }
+    return MVG_OK;
+}
+
 // Exact mode's column-panel copy of a shard (s.panelP > 0), allocated when first needed if it
 // fits in free HBM with 8 GiB to spare; otherwise the shard keeps the row-major exact kernels
 // (panelP = 0 until exact mode is switched on again).
@@ -270,32 +344,34 @@ int distribute_direct(mvg_engine* e, const double* A, const double* x) {
     return MVG_OK;
 }
 
-// The exchange step from the shared schedule (mvg_plan_exchange). A failing call inside the
-// group still closes the group before the error is reported.
-int exchange_plan(mvg_engine* e, int b, bool serial) {
+// The exchange step from the shared schedule (mvg_plan_exchange): one group per step, every
+// local member issuing its call in it. A failing call inside the group still closes the group
+// before the error is reported.
+int exchange_plan(mvg_engine* e, int b, bool serial, XOps& ops) {
     const int nsteps = e->shards[0].nsteps;
     for (int k = 0; k < nsteps; ++k) {
-        MVG_NCCL(ncclGroupStart());
+        MVG_NCCL(ops.group_start());
         ncclResult_t r = ncclSuccess;
         const char* what = "";
         for (auto& s : e->shards) {
             const mvg_xstep& st = s.steps[k];
             if (!st.member) continue;
-            (void)hipSetDevice(s.device);
+            ops.set_device(s.device);
             double* bufs[3] = {s.dy_parts[b], s.dy_row, s.dy};
             const double* src = bufs[st.src];
             double* dst = bufs[st.dst];
             if (!dst) dst = s.dy_parts[b];  // recvbuff is only written on the root
+            hipStream_t stream = serial ? s.stream : s.xstream;
             if (st.op == MVG_X_GATHER) {
-                r = ncclGather(src, dst, (size_t)st.count, ncclFloat64, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
+                r = ops.gather(src, dst, (size_t)st.count, st.root, s.xcomm[k], stream);
                 what = "ncclGather";
             } else {
-                r = ncclReduce(src, dst, (size_t)st.count, ncclFloat64, ncclSum, st.root, s.xcomm[k], serial ? s.stream : s.xstream);
+                r = ops.reduce(src, dst, (size_t)st.count, st.root, s.xcomm[k], stream);
                 what = "ncclReduce";
             }
             if (r != ncclSuccess) break;
         }
-        const ncclResult_t r2 = ncclGroupEnd();
+        const ncclResult_t r2 = ops.group_end();
         if (r != ncclSuccess) return nccl_fail(r, what);
         if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
     }
@@ -304,32 +380,104 @@ int exchange_plan(mvg_engine* e, int b, bool serial) {
 
 // Exact mode (mvg_engine_set_exact): every partial gathered to rank 0 in rank order, then added
 // there in the reference's order.
-int exchange_exact(mvg_engine* e, int b, bool serial) {
+int exchange_exact(mvg_engine* e, int b, bool serial, XOps& ops) {
     const int64_t count = e->alg == MVG_ALG_COLWISE ? e->R : e->shards[0].plan.y_len;
-    MVG_NCCL(ncclGroupStart());
+    MVG_NCCL(ops.group_start());
     ncclResult_t r = ncclSuccess;
     for (auto& s : e->shards) {
-        (void)hipSetDevice(s.device);
+        ops.set_device(s.device);
         // recvbuff is only written on the root
-        r = ncclGather(s.dy_parts[b], s.rank == 0 ? s.gbuf : s.dy_parts[b], (size_t)count, ncclFloat64, 0,
-                       s.world, serial ? s.stream : s.xstream);
+        r = ops.gather(s.dy_parts[b], s.rank == 0 ? s.gbuf : s.dy_parts[b], (size_t)count, 0, s.world,
+                       serial ? s.stream : s.xstream);
         if (r != ncclSuccess) break;
     }
-    const ncclResult_t r2 = ncclGroupEnd();
+    const ncclResult_t r2 = ops.group_end();
     if (r != ncclSuccess) return nccl_fail(r, "ncclGather (exact)");
     if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
     for (auto& s : e->shards) {
         if (s.rank != 0) continue;
-        MVG_HIP(hipSetDevice(s.device));
-        hipStream_t st = serial ? s.stream : s.xstream;
-        const int rc = e->alg == MVG_ALG_COLWISE
-                           ? launch_combine_mpich_reduce(s.gbuf, e->nranks, e->R, s.dy, st)
-                           : launch_combine_grid_rows(s.gbuf, s.plan.grid_rows, s.plan.grid_cols, s.plan.y_len,
-                                                      s.dy, st);
+        ops.set_device(s.device);
+        const int rc = ops.combine(e, s, serial ? s.stream : s.xstream);
         if (rc != MVG_OK) return rc;
     }
     return MVG_OK;
 }
+
+// The recorder behind mvg_debug_trace_exchange. Communicators and buffers are stand-in handles
+// the trace hands out; every call is listed with the group it was issued in.
+struct TraceXOps final : XOps {
+    std::vector<mvg_xcall> calls;
+    int group = -1, depth = 0, device = 0;
+    std::vector<std::pair<uintptr_t, int>> comm_step;  // handle -> group that created it (-1 world)
+    std::vector<std::pair<uintptr_t, std::pair<int, int>>> buffers;  // address -> (rank, MVG_X_BUF_*)
+    uintptr_t next_comm = 0x7e0000;
+
+    int comm_of(ncclComm_t c) const {
+        for (auto& kv : comm_step)
+            if (kv.first == (uintptr_t)c) return kv.second;
+        return -2;
+    }
+    int buf_of(const double* p) const {
+        for (auto& kv : buffers)
+            if (kv.first == (uintptr_t)p) return kv.second.second;
+        return -1;
+    }
+    mvg_xcall base(int kind) const {
+        mvg_xcall c{};
+        c.group = depth > 0 ? group : -1;  // -1: outside any group (the combine kernel)
+        c.kind = kind;
+        c.rank = device;  // the trace's devices are its ranks
+        c.comm = -1;
+        c.color = c.key = c.root = -1;
+        c.src = c.dst = -1;
+        return c;
+    }
+    ncclResult_t group_start() override {
+        if (depth++ == 0) ++group;
+        return ncclSuccess;
+    }
+    ncclResult_t group_end() override {
+        if (depth > 0) --depth;
+        return ncclSuccess;
+    }
+    void set_device(int dev) override { device = dev; }
+    ncclResult_t split(ncclComm_t world, int color, int key, ncclComm_t* out) override {
+        mvg_xcall c = base(MVG_XCALL_SPLIT);
+        c.comm = comm_of(world);
+        c.color = color == NCCL_SPLIT_NOCOLOR ? -1 : color;
+        c.key = key;
+        calls.push_back(c);
+        *out = (ncclComm_t)(next_comm++);
+        comm_step.push_back({(uintptr_t)*out, group});
+        return ncclSuccess;
+    }
+    ncclResult_t coll(int kind, const double* src, double* dst, size_t count, int root, ncclComm_t comm) {
+        mvg_xcall c = base(kind);
+        c.comm = comm_of(comm);
+        c.root = root;
+        c.count = (int64_t)count;
+        c.src = buf_of(src);
+        c.dst = buf_of(dst);
+        calls.push_back(c);
+        return ncclSuccess;
+    }
+    ncclResult_t gather(const double* src, double* dst, size_t count, int root, ncclComm_t comm,
+                        hipStream_t) override {
+        return coll(MVG_XCALL_GATHER, src, dst, count, root, comm);
+    }
+    ncclResult_t reduce(const double* src, double* dst, size_t count, int root, ncclComm_t comm,
+                        hipStream_t) override {
+        return coll(MVG_XCALL_REDUCE, src, dst, count, root, comm);
+    }
+    int combine(const mvg_engine* e, const Shard& s, hipStream_t) override {
+        mvg_xcall c = base(MVG_XCALL_COMBINE);
+        c.count = (e->alg == MVG_ALG_COLWISE ? e->R : s.plan.y_len) * e->nranks;
+        c.src = buf_of(s.gbuf);
+        c.dst = buf_of(s.dy);
+        calls.push_back(c);
+        return MVG_OK;
+    }
+};
 
 }  // namespace
 
@@ -483,10 +631,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
                     hipEventCreateWithFlags(&s.x_done[b], hipEventDisableTiming) != hipSuccess)
                     return bail(fail(MVG_E_HIP, "hipEventCreate"));
         }
-        bool need_row = false;
-        for (int k = 0; k < s.nsteps; ++k)
-            need_row |= s.steps[k].member && (s.steps[k].dst == MVG_X_BUF_ROW || s.steps[k].src == MVG_X_BUF_ROW);
-        if (need_row)
+        if (needs_row_buffer(s))
             if ((rc = alloc_doubles(&s.dy_row, p.y_len)) != MVG_OK) return bail(rc);
         if (l.rank == 0)
             if ((rc = alloc_doubles(&s.dy, R)) != MVG_OK) return bail(rc);
@@ -530,26 +675,7 @@ int mvg_engine_create(mvg_engine** out, int alg, int64_t R, int64_t C, mvg_comm*
         (void)hipHostFree(pinned);
         if (we != hipSuccess) return bail(hip_fail(we, "engine warm-up"));
     }
-    // Sub-communicators of the exchange schedule. ncclCommSplit is collective over the world,
-    // so every local rank calls it for every split step, inside one group per step.
-    const int nsteps = e->shards[0].nsteps;
-    for (int k = 0; k < nsteps; ++k) {
-        if (e->shards[0].steps[k].comm == MVG_X_WORLD) {
-            for (auto& s : e->shards) s.xcomm[k] = s.world;
-            continue;
-        }
-        ncclResult_t r = ncclGroupStart();
-        for (auto& s : e->shards) {
-            if (r != ncclSuccess) break;
-            (void)hipSetDevice(s.device);
-            const mvg_xstep& st = s.steps[k];
-            r = ncclCommSplit(s.world, st.member ? st.color : NCCL_SPLIT_NOCOLOR, st.key, &s.xcomm[k], nullptr);
-            s.owns_xcomm[k] = true;
-        }
-        ncclResult_t r2 = ncclGroupEnd();
-        if (r != ncclSuccess) return bail(nccl_fail(r, "ncclCommSplit"));
-        if (r2 != ncclSuccess) return bail(nccl_fail(r2, "ncclCommSplit group"));
-    }
+    if ((rc = split_steps(e->shards, g_device_ops)) != MVG_OK) return bail(rc);
     if (want_exact && (rc = mvg_engine_set_exact(e, 1)) != MVG_OK) return bail(rc);
     *out = e;
     return MVG_OK;
@@ -860,7 +986,8 @@ int mvg_engine_multiply(mvg_engine* e) {
     }
     if (solo) return MVG_OK;
     // 2) the exchange step on the exchange stream, overlapping the next multiply's GEMV
-    const int rc_x = e->exact && e->alg != MVG_ALG_ROWWISE ? exchange_exact(e, b, serial) : exchange_plan(e, b, serial);
+    const int rc_x = e->exact && e->alg != MVG_ALG_ROWWISE ? exchange_exact(e, b, serial, g_device_ops)
+                                                            : exchange_plan(e, b, serial, g_device_ops);
     if (rc_x != MVG_OK) return rc_x;
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
@@ -922,6 +1049,55 @@ int mvg_engine_collect(mvg_engine* e, double* y) {
             MVG_HIP(hipMemcpyAsync(y, s.dy, (size_t)e->R * sizeof(double), hipMemcpyDeviceToHost, s.stream));
         MVG_HIP(hipStreamSynchronize(s.stream));
     }
+    return MVG_OK;
+}
+
+// The single-process G-device exchange (the executables' MVG_NGPUS=G form) without devices:
+// the shards the engine would create over G local devices (the same planner, the same buffer
+// choices), their communicator splits and one multiply's exchange, issued through the recorder
+// instead of RCCL (split_steps, exchange_plan / exchange_exact: the engine's own code).
+int mvg_debug_trace_exchange(int alg, int64_t R, int64_t C, int ndev, int exact, mvg_xcall* calls, int max_calls,
+                             int* ncalls) {
+    if (!calls || !ncalls || ndev <= 0 || max_calls < 0) return fail(MVG_E_INVALID, "mvg_debug_trace_exchange: bad arguments");
+    *ncalls = 0;
+    mvg_shard probe;
+    int rc = mvg_plan_shard(alg, R, C, ndev, 0, &probe);
+    if (rc != MVG_OK) return rc;
+    mvg_engine e;
+    e.alg = alg;
+    e.R = R;
+    e.C = C;
+    e.nranks = ndev;
+    e.single_process = true;
+    e.exact = exact != 0;
+    e.shards.resize(ndev);
+    TraceXOps ops;
+    auto fake = [&](int r, int id) {
+        const uintptr_t a = ((uintptr_t)(r + 1) << 24) + ((uintptr_t)(id + 1) << 16);
+        ops.buffers.push_back({a, {r, id}});
+        return (double*)a;
+    };
+    for (int r = 0; r < ndev; ++r) {
+        Shard& s = e.shards[r];
+        s.device = r;
+        s.rank = r;
+        s.world = (ncclComm_t)((uintptr_t)0x7d0000 + r);
+        ops.comm_step.push_back({(uintptr_t)s.world, -1});
+        if ((rc = mvg_plan_shard(alg, R, C, ndev, r, &s.plan)) != MVG_OK) return rc;
+        if ((rc = mvg_plan_exchange(alg, R, C, ndev, r, 0, s.steps, MVG_MAX_XSTEPS, &s.nsteps)) != MVG_OK) return rc;
+        s.dy_parts[0] = fake(r, MVG_X_BUF_PART);
+        if (needs_row_buffer(s)) s.dy_row = fake(r, MVG_X_BUF_ROW);
+        if (r == 0) s.dy = fake(r, MVG_X_BUF_Y);
+        if (e.exact && alg != MVG_ALG_ROWWISE && r == 0 && s.nsteps > 0) s.gbuf = fake(r, MVG_X_BUF_GATHERED);
+    }
+    if ((rc = split_steps(e.shards, ops)) != MVG_OK) return rc;
+    if (e.shards[0].nsteps > 0) {
+        rc = e.exact && alg != MVG_ALG_ROWWISE ? exchange_exact(&e, 0, false, ops) : exchange_plan(&e, 0, false, ops);
+        if (rc != MVG_OK) return rc;
+    }
+    if ((int)ops.calls.size() > max_calls) return fail(MVG_E_INVALID, "mvg_debug_trace_exchange: calls buffer too small");
+    for (size_t i = 0; i < ops.calls.size(); ++i) calls[i] = ops.calls[i];
+    *ncalls = (int)ops.calls.size();
     return MVG_OK;
 }
 

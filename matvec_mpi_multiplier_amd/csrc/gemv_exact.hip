@@ -788,13 +788,29 @@ constexpr int kMi355xCUs = 256;  // when no device answers (host-only callers, t
 // the rows (64-row workgroups a multiple of the CU count: the BASELINE configs' 16384-row
 // multiples) and K < 65536; a partial last round costs a whole round (24576 x 16384: 541 against
 // 470 us), and at 131072^2 the 24-segment one-wave form stays 2 % ahead (19.64 against 20.03 ms).
-static int device_cu_count() {
-    static std::atomic<int> cached[64];
+// Test hooks (mvg_debug_*, include/matvec_gpu.h): a CU count standing in for the device's, and
+// an LDS reservation for the evenly placed form that a runtime must refuse (above the CU's
+// 160 KiB) to drive the refusal fallback below.
+static std::atomic<int> g_cu_override{0};
+static std::atomic<int64_t> g_even_lds_override{0};
+// Per device: the runtime refused the evenly placed form's LDS reservation once; the dispatch
+// then keeps to the one-wave forms on that device (no failing launch per call).
+static std::atomic<int> g_even_refused[64];
+
+static int current_device() {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
         (void)hipGetLastError();
-        return kMi355xCUs;
+        return -1;
     }
+    return dev;
+}
+
+static int device_cu_count() {
+    static std::atomic<int> cached[64];
+    if (const int o = g_cu_override.load(std::memory_order_relaxed); o > 0) return o;
+    const int dev = current_device();
+    if (dev < 0) return kMi355xCUs;
     int n = cached[dev].load(std::memory_order_relaxed);
     if (n > 0) return n;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
@@ -805,10 +821,22 @@ static int device_cu_count() {
     return n;
 }
 
+static bool even_refused() {
+    const int dev = current_device();
+    return dev >= 0 && g_even_refused[dev].load(std::memory_order_relaxed) != 0;
+}
+
+// The errors with which the runtime turns down a launch's resources before dispatching it (the
+// LDS request above the CU's, a workgroup it cannot place); profiles/r05/p5a/lds_refusal.txt.
+static bool launch_refused(hipError_t e) {
+    return e == hipErrorInvalidValue || e == hipErrorInvalidConfiguration || e == hipErrorLaunchOutOfResources ||
+           e == hipErrorOutOfMemory;
+}
+
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
     if (lines && operands_ok(kVec16Lda23, lda, aligned) && M >= 32768 && K > 2048 && K < 65536)
         return kSeqManyRows;
-    if (M >= 6144 && K > kShortRowK && K < 65536) {
+    if (M >= 6144 && K > kShortRowK && K < 65536 && !even_refused()) {
         const int64_t wgs = (M + 63) / 64, cus = device_cu_count();
         if (wgs >= cus && wgs % cus == 0) return kHopEven;
     }
@@ -898,19 +926,41 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         cap = cap / var.rows * var.rows;
         if (cap < max_rows) max_rows = cap;
     }
-    const size_t lds = var.xlds ? (size_t)k * sizeof(double) : (size_t)var.lds_reserve;
+    size_t lds = var.xlds ? (size_t)k * sizeof(double) : (size_t)var.lds_reserve;
+    if (v == kHopEven)
+        if (const int64_t o = g_even_lds_override.load(std::memory_order_relaxed); o > 0) lds = (size_t)o;
+    // An error an earlier call left pending is that call's: reported here as it is (this call
+    // fails, nothing launched), never mistaken for a refusal of this launch below.
+    if (const hipError_t pending = hipGetLastError(); pending != hipSuccess)
+        return hip_fail(pending, "mvg_gemv_exact: HIP error pending from an earlier call");
     for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
         const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
         const int rw = var.rows;
         hipLaunchKernelGGL(var.fn, dim3((unsigned)((mm + rw - 1) / rw)), dim3(64 * var.waves), lds, s,
                            A ? A + r0 * lda : A, lda, x, y + r0, mm, k);
         const hipError_t e = hipGetLastError();
-        // a runtime that refuses the evenly placed form's LDS reservation gets the same sums from
-        // the one-wave form (the whole call: nothing of it has been launched yet)
-        if (e != hipSuccess && variant == 0 && v == kHopEven && r0 == 0)
+        // A runtime that turns down the evenly placed form's LDS reservation (the first launch of
+        // the call, nothing of it dispatched) gets the same sums from the one-wave form, and the
+        // dispatch keeps to the one-wave forms on this device from then on.
+        if (e != hipSuccess && variant == 0 && v == kHopEven && r0 == 0 && launch_refused(e)) {
+            if (const int dev = current_device(); dev >= 0) g_even_refused[dev].store(1, std::memory_order_relaxed);
             return mvg_gemv_exact_variant(A, lda, x, y, m, k, kHopRows, stream);
+        }
         MVG_HIP(e);
     }
+    return MVG_OK;
+}
+
+int mvg_debug_set_cu_count(int n) {
+    if (n < 0) return fail(MVG_E_INVALID, "mvg_debug_set_cu_count: negative count");
+    g_cu_override.store(n, std::memory_order_relaxed);
+    return MVG_OK;
+}
+
+int mvg_debug_set_exact_even_lds(int64_t bytes) {
+    if (bytes < 0) return fail(MVG_E_INVALID, "mvg_debug_set_exact_even_lds: negative size");
+    g_even_lds_override.store(bytes, std::memory_order_relaxed);
+    for (auto& f : g_even_refused) f.store(0, std::memory_order_relaxed);
     return MVG_OK;
 }
 

@@ -53,6 +53,17 @@ def plan_exchange(alg, R: int, Cn: int, nranks: int, rank: int, force_collect: b
 
 
 # ------------------------------------------------------------------ text I/O
+def trace_exchange(alg, R: int, Cn: int, ndev: int, exact: bool = False) -> list[dict]:
+    """The calls one process driving `ndev` devices issues for the exchange (communicator splits,
+    then one multiply's collectives; mvg_debug_trace_exchange), as dicts in issue order."""
+    cap = 16 * ndev + 16
+    calls = (_lib.XCall * cap)()
+    n = C.c_int()
+    check(lib.mvg_debug_trace_exchange(_alg_id(alg), R, Cn, ndev, int(exact), calls, cap, C.byref(n)),
+          "mvg_debug_trace_exchange")
+    return [calls[i].as_dict() for i in range(n.value)]
+
+
 def build_matrix_filename(R: int, Cn: int) -> str:
     buf = C.create_string_buffer(128)
     check(lib.mvg_matrix_filename(R, Cn, buf, 128), "mvg_matrix_filename")

@@ -197,6 +197,7 @@ def test_kernel_family_names():
     assert bench.kernel_family("rowblk_w8_r2_u4_splitk") == "gemv_rowblock_split"
     assert bench.kernel_family("vec_l64_r1_u4_nt1_o5") == "gemv_vec"
     assert bench.kernel_family("hop8_l8_w2_u16") == "gemv_seq_hop"
+    assert bench.kernel_family("hop8e_l8_w2_u16_n8") == "gemv_seq_hop_n8"  # not the one-wave form's counters
     assert bench.kernel_family("hopxl_l8_w2_u16_n4") == "gemv_seq_hop_xl"
     assert bench.kernel_family("seqx_r64_t16_b2_g8") == "gemv_seq_x"
     assert bench.kernel_family("panel_l8_w2_u16 (column panels, P = 256)") == "gemv_seq_hop_panel"
@@ -258,3 +259,162 @@ def test_ref_sweep_reports_speedup_and_efficiency(monkeypatch):
     assert pts[1]["speedup"] == 1.0 and pts[2]["speedup"] == round(0.05 / 0.03, 3)
     assert pts[16]["efficiency"] == round(0.05 / 0.04 / 16, 3) and pts[16]["placement"] == "compact"
     assert out["errors"] and "P=8" in out["errors"][0]
+
+
+# ---- the wall-time budget and the truncated line (a time limit must not lose the scaling line)
+
+def test_budget_skips_a_section_that_does_not_fit_and_records_times():
+    b = bench.Budget(limit_s=bench.Budget(0).used() + 5.0)  # about 5 s left
+    ran = []
+    assert b.run("quick", 0.5, lambda v: ran.append(v) or v, 7) == 7
+    got = b.run("huge", 3600.0, lambda: ran.append("huge"))
+    assert ran == [7] and got["skipped"] == "budget" and got["need_s"] == 3600.0 and 0 < got["left_s"] <= 5
+    assert set(b.sections) == {"quick"} and b.skipped == ["huge"]
+    rec = b.record()
+    assert rec["skipped"] == ["huge"] and rec["limit_s"] == b.limit_s
+    # nested sections name the innermost one in progress, then restore the outer one
+    seen = []
+    b.run("outer", 0.0, lambda: b.run("inner", 0.0, lambda: seen.append(b.current)) or seen.append(b.current))
+    assert seen == ["inner", "outer"] and b.current is None
+
+
+def _budget_rank(rank, world, port, out):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 1 is short of time, rank 0 is not: both must skip (no rank left waiting)
+        b = bench.Budget(1e6 if rank == 0 else 0.0, distributed=True, device="cpu")
+        got = b.run("section", 1.0, lambda: "ran")
+        out.put((rank, got if isinstance(got, str) else got["skipped"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_budget_decision_is_all_reduced_over_ranks():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_budget_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == {0: "budget", 1: "budget"}
+
+
+def test_report_writes_one_line_with_sections_and_warnings(tmp_path):
+    import io
+
+    buf = io.StringIO()
+    b = bench.Budget(1e6)
+    r = bench.Report(buf, b)
+    r.update({"metric": bench.METRIC, "value": 1.5})
+    b.run("configs", 0.0, lambda: r.append("configs", {"config": "config 3"}))
+    bench.WARNINGS.append("single_process: failed")
+    try:
+        assert r.write() is True and r.write() is False  # once only
+    finally:
+        bench.WARNINGS.clear()
+    lines = buf.getvalue().splitlines()
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] == 1.5 and d["configs"] == [{"config": "config 3"}] and "configs" in d["sections_s"]
+    assert d["warnings"] == ["single_process: failed"] and d["failures"] is None and "truncated" not in d
+
+
+_BLOCKED_RANK0 = r'''
+import ctypes, os, sys, time
+sys.path.insert(0, {repo!r})
+import bench
+b = bench.Budget(1e6)
+r = bench.Report(sys.stdout, b)
+r.update({{"metric": bench.METRIC, "value": 7166.9}})
+r.watch_signals()
+r["exact"] = {{"value": 1.0}}
+b.sections["headline"] = 0.3
+def blocked():
+    open({marker!r}, "w").write("in")
+    ctypes.CDLL(None).sleep(60)  # the main thread inside a C call: no Python handler can run
+b.run("config 4 end_to_end", 0.0, blocked)
+print("not reached")
+'''
+
+
+def _start_blocked(tmp_path, wrap_in_relay):
+    child = tmp_path / "rank0.py"
+    marker = tmp_path / "marker"
+    child.write_text(_BLOCKED_RANK0.format(repo=REPO, marker=str(marker)))
+    if wrap_in_relay:
+        parent = tmp_path / "relay.py"
+        parent.write_text(f"import sys\nsys.path.insert(0, {REPO!r})\nimport bench\n"
+                          f"sys.exit(bench.relay([sys.executable, {str(child)!r}]))\n")
+        cmd = [sys.executable, str(parent)]
+    else:
+        cmd = [sys.executable, str(child)]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    import time
+
+    for _ in range(300):
+        if marker.exists():
+            break
+        time.sleep(0.1)
+    assert marker.exists(), p.communicate(timeout=5)
+    return p
+
+
+@pytest.mark.parametrize("wrap_in_relay", [False, True])
+def test_sigterm_mid_section_writes_the_truncated_line(tmp_path, wrap_in_relay):
+    """A SIGTERM while rank 0's main thread is blocked in a C call (a GPU copy, the oracle):
+    the watcher thread still writes the line so far, marked truncated, and the process exits
+    128 + 15. Through the launcher-free relay (`bench.py --gpus N`) the same line comes out."""
+    import signal
+
+    p = _start_blocked(tmp_path, wrap_in_relay)
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=60)
+    assert p.returncode == 128 + signal.SIGTERM, err
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in out, out
+    d = json.loads(lines[0])
+    assert d["truncated"] is True and d["truncated_by"] == "SIGTERM"
+    assert d["truncated_in"] == "config 4 end_to_end"
+    assert d["value"] == 7166.9 and d["exact"] == {"value": 1.0} and d["sections_s"]["headline"] == 0.3
+
+
+def test_host_rows_region_is_page_aligned_within_the_matrix():
+    A = np.zeros((1000, 513))
+    lo, n = bench.host_rows_region(A, 100, 300)
+    base, end = A.ctypes.data, A.ctypes.data + A.nbytes
+    assert lo % 4096 == 0 or lo == base
+    assert base <= lo <= base + 100 * 513 * 8 and lo + n >= base + 300 * 513 * 8 and lo + n <= end
+    assert (lo + n) % 4096 == 0 or lo + n == end
+
+
+def test_host_memory_and_cache_probes():
+    assert bench.host_mem_free() > 0
+    c = bench.host_cache()
+    if c is not None:  # sysfs exposes the L3 on this host
+        assert c["l3_bytes"] >= c["l3_instance_bytes"] > 0 and c["l3_bytes_system"] >= c["l3_bytes"]
+    class A:
+        pass
+    rows = bench.big_sample_rows(A(), "rowwise", 16384, 16384)
+    assert 8 * rows * 16384 >= max(1 << 30, 2 * ((c or {}).get("l3_bytes_system") or 0)) and rows <= 16384
+
+
+def test_section_estimates_grow_with_the_work():
+    assert bench.est_e2e(137e9, 1, 3, False) > bench.est_e2e(2.1e9, 1, 3, False) > 4
+    assert bench.est_e2e(17e9, 8, 3, True) > bench.est_e2e(17e9, 8, 3, False)
+    class A:
+        ref_rows, cpu_sample_bytes, cpu_seconds = 1024, 2.2e9, 12.0
+    small = bench.est_cpu_baseline(A(), 16384, 16384)
+    assert bench.est_cpu_baseline(A(), 16384, 16384, big_rows=8192) > small > 24

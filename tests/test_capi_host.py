@@ -446,11 +446,21 @@ def test_multi_vector_dispatch_takes_dma_forms_on_long_rows():
     assert not name(4200, 4200, 16).startswith("m16")
 
 
-def test_exact_row_major_dispatch():
-    """pick_seq_variant (host logic; with no GPU the CU count is the MI355X's 256): the LDS form for
-    line-aligned tall rows, the evenly placed 8-lane form where whole rounds of one 8-wave
-    workgroup per CU cover the rows (16384·k rows, 768 < K < 65536), the one-wave 8-lane forms
-    otherwise (partial rounds, short rows, K >= 65536), wider lane groups for few rows."""
+@pytest.fixture
+def cu_count():
+    """The exact dispatch's CU count set through its test hook (mvg_debug_set_cu_count), put back
+    to the device's afterwards."""
+    yield lambda n: _lib.check(_lib.lib.mvg_debug_set_cu_count(n), "mvg_debug_set_cu_count")
+    _lib.lib.mvg_debug_set_cu_count(0)
+
+
+def test_exact_row_major_dispatch(cu_count):
+    """pick_seq_variant (host logic) at the MI355X's 256 CUs, set explicitly (the device's own
+    count on a GPU box, which a partitioned mode would change): the LDS form for line-aligned tall
+    rows, the evenly placed 8-lane form where whole rounds of one 8-wave workgroup per CU cover
+    the rows (16384·k rows, 768 < K < 65536), the one-wave 8-lane forms otherwise (partial rounds,
+    short rows, K >= 65536), wider lane groups for few rows."""
+    cu_count(256)
     name = lambda m, k, lda=None: _lib.lib.mvg_gemv_exact_variant_name(  # noqa: E731
         _lib.lib.mvg_gemv_exact_auto_variant(lda or k, m, k)).decode()
     assert name(16384, 16384) == "hop8e_l8_w2_u16_n8"     # config 2 (and its weak-scaled shards)
@@ -463,3 +473,16 @@ def test_exact_row_major_dispatch():
     assert name(524288, 512) == "hop8_l8_w2_u16"          # short rows want more waves per CU
     assert name(4194304, 512) == "hop8_l8_w2_u16"
     assert name(1200, 60000).startswith("hop8_l32")       # few long rows: the chain dominates
+
+
+@pytest.mark.parametrize("cus", [256, 32, 100])
+def test_exact_even_form_needs_whole_rounds_of_workgroups(cu_count, cus):
+    """The evenly placed form's rule on its own: 64-row workgroups, one per CU per round, so it
+    is taken exactly when the workgroup count is a positive multiple of the CU count (and
+    768 < K < 65536, >= 6144 rows, no LDS form)."""
+    cu_count(cus)
+    for m in (6144, 8192, 16384, 24576, 32768 + 64, 49152):
+        v = _lib.lib.mvg_gemv_exact_variant_name(_lib.lib.mvg_gemv_exact_auto_variant(16383, m, 16383)).decode()
+        wgs = -(-m // 64)
+        assert (v == "hop8e_l8_w2_u16_n8") == (wgs >= cus and wgs % cus == 0), (m, cus, v)
+

@@ -402,3 +402,68 @@ def test_engine_exact_panels_fill_synth_and_toggle(comm1):
     for r in [0, 1, 7, 8, R // 2, R - 1]:
         Ar = oracle.synth_block(r, 1, 0, Cn, Cn, mm.SEED_A)
         assert oracle.multiply_std_rowwise(Ar, x)[0] == y1[r], r
+
+
+def _hip_runtime():
+    """The HIP runtime this process already has loaded (the library's), through ctypes."""
+    import ctypes
+
+    for line in open("/proc/self/maps"):
+        if "libamdhip64.so" in line:
+            return ctypes.CDLL(line.split()[-1])
+    raise AssertionError("libamdhip64 is not loaded")
+
+
+@pytest.fixture
+def exact_hooks():
+    lib = _lib.lib
+    yield lib
+    lib.mvg_debug_set_cu_count(0)
+    lib.mvg_debug_set_exact_even_lds(0)
+
+
+def test_exact_dispatch_falls_back_when_the_runtime_refuses_the_lds_reservation(exact_hooks):
+    """The evenly placed form reserves LDS to place one 8-wave workgroup per CU. A runtime that
+    turns the reservation down (forced here: 200 KiB, above the CU's 160 KiB) gets the one-wave
+    form's sums — the reference's, bit for bit — and the dispatch keeps to the one-wave form on
+    the device from then on (auto_variant says so; no failing launch per call)."""
+    lib = exact_hooks
+    _lib.check(lib.mvg_debug_set_cu_count(32), "cu count")  # 6144 rows = 96 workgroups = 3 rounds
+    m, k = 6144, 1000
+    name = lambda: lib.mvg_gemv_exact_variant_name(lib.mvg_gemv_exact_auto_variant(k, m, k)).decode()  # noqa: E731
+    assert name() == "hop8e_l8_w2_u16_n8"
+    A = signed(oracle.synth(m, k, 42), 5)
+    x = signed(oracle.synth(1, k, 4242)[0], 6)
+    want = oracle.multiply_std_rowwise(A, x)
+    assert np.array_equal(mm.multiply_std_rowwise(A, x, exact=True), want)  # the even form itself
+    _lib.check(lib.mvg_debug_set_exact_even_lds(200 * 1024), "even lds")
+    assert name() == "hop8e_l8_w2_u16_n8"  # not refused yet
+    y = mm.multiply_std_rowwise(A, x, exact=True)
+    assert np.array_equal(y, want), max_rel(y, want)
+    assert name() == "hop8_l8_w2_u16"  # the refusal is remembered for this device
+    assert np.array_equal(mm.multiply_std_rowwise(A, x, exact=True), want)
+    _lib.check(lib.mvg_debug_set_exact_even_lds(0), "even lds")  # forgets the refusal
+    assert name() == "hop8e_l8_w2_u16_n8"
+
+
+def test_exact_call_reports_an_error_pending_from_an_earlier_call(exact_hooks):
+    """An error an earlier HIP call left pending is returned by the next exact call as a
+    failure (never taken for a refused launch and silently re-dispatched); the call after that
+    runs normally."""
+    lib = exact_hooks
+    m, k = 6144, 1000
+    A = oracle.synth(m, k, 42)
+    x = oracle.synth(1, k, 4242)[0]
+    dA, dx, dy = mm.DeviceBuffer(m * k).upload(A), mm.DeviceBuffer(k).upload(x), mm.DeviceBuffer(m)
+    try:
+        _lib.check(lib.mvg_stream_sync(None), "sync")
+        hip = _hip_runtime()
+        assert hip.hipSetDevice(1 << 20) != 0  # no such device: leaves an error pending
+        rc = lib.mvg_gemv_exact(dA.ptr, k, dx.ptr, dy.ptr, m, k, None)
+        assert rc != 0 and "pending" in lib.mvg_last_error().decode()
+        _lib.check(lib.mvg_gemv_exact(dA.ptr, k, dx.ptr, dy.ptr, m, k, None), "mvg_gemv_exact")
+        _lib.check(lib.mvg_stream_sync(None), "sync")
+        assert np.array_equal(dy.download(m), oracle.multiply_std_rowwise(A, x))
+    finally:
+        for b in (dA, dx, dy):
+            b.free()

@@ -1,0 +1,47 @@
+# Round-5 check on one MI355X (gpurun, repo root). Steps chosen by STEPS (default
+# "probe tests smoke bench"); output in gpurun_out/$OUT. Every GPU step runs under its own time
+# limit; a test failure (rc 1) lets the later steps run, anything else (a fault, an abort, a
+# time limit) ends the script there.
+set -o pipefail
+OUT=gpurun_out/${OUT:-r5a}
+STEPS=${STEPS:-"probe tests smoke bench"}
+TESTS=${TESTS:-tests}
+ROOT=$PWD
+mkdir -p $OUT
+export TMPDIR=/tmp
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+for step in $STEPS; do
+  case $step in
+  probe)
+    echo "== lds refusal probe"
+    timeout -k 10 60 ./tools/probes/lds_refusal > $OUT/lds_refusal.txt 2>&1; rc=$?
+    cat $OUT/lds_refusal.txt; [ $rc -eq 0 ] || exit $rc
+    (grep -E "MemTotal|MemAvailable" /proc/meminfo; cat /sys/fs/cgroup/memory.max /sys/fs/cgroup/memory.current;
+     df -B1 /dev/shm; for i in /sys/devices/system/cpu/cpu0/cache/index*; do echo $i $(cat $i/level $i/type $i/size $i/shared_cpu_list); done;
+     nproc; cat /sys/fs/cgroup/cpu.max; lscpu | grep -iE "model name|socket|L3|NUMA node") > $OUT/host.txt 2>&1
+    cat $OUT/host.txt ;;
+  tests)
+    echo "== pytest gpu ($TESTS)"
+    timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+    rc=$?; tail -5 $OUT/pytest_gpu.log; ok $rc || exit $rc ;;
+  smoke)
+    echo "== smoke"
+    timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
+    tail -2 $OUT/smoke.log; ok $rc || exit $rc ;;
+  bench)
+    echo "== bench N=1 (the driver's command)"
+    timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; rc=$?
+    tail -c 300 $OUT/bench.json; tail -3 $OUT/bench.err; ok $rc || exit $rc ;;
+  benchprof)
+    echo "== bench N=1 under rocprofv3 --kernel-trace --stats"
+    cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof -o run -- \
+        python3 $ROOT/bench.py --steps 20 --warmup 5 > $ROOT/$OUT/bench_prof.json 2> $ROOT/$OUT/bench_prof.err; rc=$?
+    cd $ROOT; ok $rc || { tail $OUT/bench_prof.err; exit $rc; }
+    python3 tools/rocprof_by_grid.py $OUT/prof --out $OUT/kernel_by_grid.csv ;;
+  rehearse8)
+    echo "== N=8 same-device rehearsal with a 150 s budget"
+    MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 150 \
+        > $OUT/bench_n8.json 2> $OUT/bench_n8.err; rc=$?
+    tail -c 400 $OUT/bench_n8.json; tail -3 $OUT/bench_n8.err; ok $rc || exit $rc ;;
+  esac
+done

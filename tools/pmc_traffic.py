@@ -36,8 +36,16 @@ CUS, XCDS = 256, 8
 
 
 def family(kernel_name: str) -> str:
-    m = re.search(r"mvg::(\w+)", kernel_name)
-    return m.group(1) if m else kernel_name.split("(")[0]
+    """The template name; the multi-wave (evenly placed) hop forms, gemv_seq_hop<L, W, U, B, NW>
+    with NW > 1, are a family of their own (gemv_seq_hop_n<NW>), as bench.kernel_family names
+    them."""
+    m = re.search(r"mvg::(\w+)(?:<([^>]*)>)?", kernel_name)
+    if not m:
+        return kernel_name.split("(")[0]
+    fam, targs = m.group(1), [a.strip() for a in (m.group(2) or "").split(",") if a.strip()]
+    if fam == "gemv_seq_hop" and len(targs) >= 5 and targs[4].isdigit() and int(targs[4]) > 1:
+        return f"{fam}_n{int(targs[4])}"
+    return fam
 
 
 def read_dirs(dirs):
