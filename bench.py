@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--config-e2e", default="3,4,5",
                     help="configs that also run the end-to-end loop, wherever host memory (and /dev/shm at "
                          "N > 1) holds their A, measured at run time; '' for none")
+    ap.add_argument("--host-mem-cap-gib", type=float, default=250.0,
+                    help="host memory the end-to-end loops may assume at most (the GPU pool caps a command near "
+                         "270 GiB, which the cgroup may not show)")
     ap.add_argument("--budget-s", type=float, default=420.0,
                     help="wall-time budget of the whole run (about 70 %% of the driver's 600 s limit): a "
                          "section whose estimate no longer fits is skipped and marked")
@@ -1036,7 +1039,7 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
             # every GPU's link, multiplied, y on the root (same values as the device-resident
             # fill, so the exact steps below still multiply the same A), wherever host memory
             # (and /dev/shm at N > 1) holds A, measured now
-            fit, mem = e2e_memory_fit(R, C, distributed, local)
+            fit, mem = e2e_memory_fit(R, C, distributed, local, cap=int(args.host_mem_cap_gib * 2 ** 30))
             if not fit:
                 e2e = {"skipped": "memory", **mem}
             else:
@@ -1112,9 +1115,20 @@ def host_mem_free() -> int:
     return max(0, free or 0)
 
 
-def e2e_memory_fit(R, C, distributed, local, margin=8 << 30):
+def process_rss() -> int:
+    try:
+        for line in open("/proc/self/status"):
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
+
+
+def e2e_memory_fit(R, C, distributed, local, margin=8 << 30, cap=None):
     """Whether the end-to-end loop's host copy of A (R x C fp64; in /dev/shm at N > 1, a
-    process's own memory at N = 1) fits with `margin` and 5 % to spare, on every rank (MIN)."""
+    process's own memory at N = 1) fits with `margin` and 5 % to spare, on every rank (MIN):
+    within the host memory measured now and, with `cap`, within cap less this process's RSS."""
     import torch
     import torch.distributed as dist
 
@@ -1122,6 +1136,8 @@ def e2e_memory_fit(R, C, distributed, local, margin=8 << 30):
 
     need = 8 * R * C
     free = host_mem_free()
+    if cap is not None:
+        free = min(free, max(0, cap - process_rss()))
     shm = shm_free_bytes() if distributed else None
     ok = free >= need * 1.05 + margin and (shm is None or shm >= need + (1 << 30))
     if distributed:

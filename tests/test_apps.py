@@ -223,7 +223,8 @@ def test_bench_two_ranks_one_device(tmp_path):
     env = dict(os.environ, MVG_SAME_DEVICE="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
-                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--e2e-iters", "1", "--config-steps", "2"],
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--e2e-iters", "1", "--config-steps", "2",
+                        "--config-e2e", "5"],
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -231,6 +232,7 @@ def test_bench_two_ranks_one_device(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["R"] == 32768 and d["config"]["bytes_per_step"] == 2 * 2147745792
     assert "mean_s" in d["end_to_end"]["root_send"]  # shared may be skipped when /dev/shm is small
+    assert d["sections_s"]["headline"] > 0 and d["budget"]["skipped"] == [] and d.get("truncated") is None
     cfg = {c["config"]: c for c in d["configs"]}
     assert cfg["config 3"]["shard"] == [65536, 32768] and cfg["config 3"]["value"] > 0
     assert cfg["config 4"]["grid"] == [1, 2] and cfg["config 4"]["shard"] == [131072, 65536]

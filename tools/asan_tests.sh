@@ -6,10 +6,10 @@
 # in place of the normal ones (MVG_LIB, MVG_ORACLE_LIB). Any ASan report or UBSan finding
 # aborts the run (halt_on_error, -fno-sanitize-recover). Python itself is not instrumented, so
 # the ASan runtime is preloaded; leak detection is off (the interpreter's own allocations).
-# Usage: tools/asan_tests.sh [log]   (default log: profiles/r04/asan_host_tests.log)
+# Usage: tools/asan_tests.sh [log]   (default log: profiles/r05/asan_host_tests.log)
 set -euo pipefail
 REPO="$(cd "$(dirname "$0")/.." && pwd)"
-LOG="${1:-$REPO/profiles/r04/asan_host_tests.log}"
+LOG="${1:-$REPO/profiles/r05/asan_host_tests.log}"
 mkdir -p "$(dirname "$LOG")"
 make -s -C "$REPO" asan
 RT="$(/opt/rocm/lib/llvm/bin/clang++ -print-file-name=libclang_rt.asan-x86_64.so)"
@@ -26,7 +26,7 @@ env MVG_LIB="$REPO/build/asan/libmatvec_gpu.so" MVG_ORACLE_LIB="$REPO/build/asan
     ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1:detect_odr_violation=0" \
     UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1" \
     LD_PRELOAD="$RT" \
-    python -m pytest tests/test_capi_host.py tests/test_oracle_golden.py tests/test_cpuset.py \
+    python -m pytest tests/test_capi_host.py tests/test_oracle_golden.py tests/test_cpuset.py tests/test_single_process_exchange.py \
         -q -p no:cacheprovider -m "not gpu" -k "not ref_runner" >> "$LOG" 2>&1
 rc=$?
 echo "# exit $rc" >> "$LOG"

@@ -38,6 +38,13 @@ for step in $STEPS; do
         python3 $ROOT/bench.py --steps 20 --warmup 5 > $ROOT/$OUT/bench_prof.json 2> $ROOT/$OUT/bench_prof.err; rc=$?
     cd $ROOT; ok $rc || { tail $OUT/bench_prof.err; exit $rc; }
     python3 tools/rocprof_by_grid.py $OUT/prof --out $OUT/kernel_by_grid.csv ;;
+  pmc)
+    echo "== PMC passes at config 2: the evenly placed exact form (the bench's row-major exact kernel) + the tree kernel beside it"
+    mkdir -p $OUT/pmc/cfg2
+    PMC_GROUPS="fetch write l2 valu mall tlb" timeout -k 10 900 bash tools/pmc_passes.sh $OUT/pmc/cfg2 16384 16384 hop8e_l8_w2_u16_n8 \
+        > $OUT/pmc_cfg2.log 2>&1; rc=$?
+    tail -3 $OUT/pmc_cfg2.log; [ $rc -eq 0 ] || exit $rc
+    python3 tools/pmc_traffic.py --outdir $OUT/pmc_summary --M 16384 --K 16384 $OUT/pmc/cfg2 ;;
   rehearse8)
     echo "== N=8 same-device rehearsal with a 150 s budget"
     MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 150 \
