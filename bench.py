@@ -162,11 +162,24 @@ class Budget:
             return self.marker(need_s)
         t0, prev = time.perf_counter(), self.current
         self.current = name
+        log(f"bench: [{self.used():.0f} s] section {name} (estimate {need_s:.0f} s)")
         try:
             return fn(*a)
         finally:
             self.sections[name] = round(time.perf_counter() - t0, 2)
+            log(f"bench: [{self.used():.0f} s] section {name} done in {self.sections[name]:.1f} s")
             self.current = prev
+
+    def heartbeat(self, every_s: float = 30.0) -> None:
+        """A progress line on stderr every `every_s` while the run lasts: a long quiet section (the
+        reference's CPU runs, a 137 GB host matrix) must not look like a hung command to a
+        supervisor that watches the output."""
+        def beat():
+            while True:
+                time.sleep(every_s)
+                log(f"bench: [{self.used():.0f} s] running: {self.current or 'between sections'}")
+
+        threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
 
     def record(self) -> dict:
         return {"limit_s": self.limit_s, "used_s": round(self.used(), 1), "skipped": list(self.skipped)}
@@ -381,6 +394,7 @@ def main():
                        "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text "
                                "inputs)"})
         report.watch_signals()
+        budget.heartbeat()
     # one process per GPU: CUDA-tensor / RCCL IPC between processes needs the dmabuf IPC mode on
     # this ROCm (the legacy handle path fails with hipIpcGetMemHandle: invalid argument); set before
     # the HIP runtime starts. With N > 1, RCCL logs at INFO to a per-rank file that rccl_report()

@@ -893,6 +893,11 @@ int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k) {
 
 int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
                            int variant, void* stream) {
+    // An error the caller's last HIP call left pending is that call's: reported here as it is
+    // (this call fails, nothing launched), before any HIP call of ours could replace it, and
+    // never mistaken for a refusal of this call's launch below.
+    if (const hipError_t pending = hipGetLastError(); pending != hipSuccess)
+        return hip_fail(pending, "mvg_gemv_exact: HIP error pending from an earlier call");
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact: negative size");
     if (variant < 0 || variant >= kNumSeqVariants || (variant > 0 && !kSeqVariants[variant].fn))
         return fail(MVG_E_INVALID, "mvg_gemv_exact: bad variant");
@@ -929,10 +934,6 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
     size_t lds = var.xlds ? (size_t)k * sizeof(double) : (size_t)var.lds_reserve;
     if (v == kHopEven)
         if (const int64_t o = g_even_lds_override.load(std::memory_order_relaxed); o > 0) lds = (size_t)o;
-    // An error an earlier call left pending is that call's: reported here as it is (this call
-    // fails, nothing launched), never mistaken for a refusal of this launch below.
-    if (const hipError_t pending = hipGetLastError(); pending != hipSuccess)
-        return hip_fail(pending, "mvg_gemv_exact: HIP error pending from an earlier call");
     for (int64_t r0 = 0; r0 < m; r0 += max_rows) {
         const int64_t mm = m - r0 < max_rows ? m - r0 : max_rows;
         const int rw = var.rows;

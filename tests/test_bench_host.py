@@ -344,7 +344,9 @@ r["exact"] = {{"value": 1.0}}
 b.sections["headline"] = 0.3
 def blocked():
     open({marker!r}, "w").write("in")
-    ctypes.CDLL(None).sleep(60)  # the main thread inside a C call: no Python handler can run
+    t0 = time.time()
+    while time.time() - t0 < 60:  # the main thread inside a C call (a signal only cuts one sleep short)
+        ctypes.CDLL(None).sleep(60)
 b.run("config 4 end_to_end", 0.0, blocked)
 print("not reached")
 '''
