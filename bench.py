@@ -134,6 +134,7 @@ class Budget:
         self.sections: dict[str, float] = {}
         self.skipped: list[str] = []
         self.current: str | None = None
+        self.failed_in: str | None = None
 
     def used(self) -> float:
         return time.perf_counter() - T_START
@@ -165,6 +166,9 @@ class Budget:
         log(f"bench: [{self.used():.0f} s] section {name} (estimate {need_s:.0f} s)")
         try:
             return fn(*a)
+        except BaseException:
+            self.failed_in = self.failed_in or name  # the innermost section an error left
+            raise
         finally:
             self.sections[name] = round(time.perf_counter() - t0, 2)
             log(f"bench: [{self.used():.0f} s] section {name} done in {self.sections[name]:.1f} s")
@@ -236,6 +240,19 @@ class Report:
             self.stream.write(json.dumps(line) + "\n")
             self.stream.flush()
         return True
+
+    def on_uncaught(self) -> None:
+        """An exception that ends the run (at N > 1 a section's error is fatal, every rank
+        must stop) still leaves the line so far, marked truncated, with the error."""
+        prev = sys.excepthook
+
+        def hook(tp, value, tb):
+            where = (self.budget.failed_in or self.budget.current) if self.budget is not None else None
+            self.write(truncated=True, truncated_by="error", truncated_in=where,
+                       error=f"{tp.__name__}: {str(value)[:300]}")
+            prev(tp, value, tb)
+
+        sys.excepthook = hook
 
     def watch_signals(self, exit_fn=None) -> None:
         """SIGTERM / SIGINT: write the line so far (truncated) and exit 128 + signal."""
@@ -394,6 +411,7 @@ def main():
                        "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text "
                                "inputs)"})
         report.watch_signals()
+        report.on_uncaught()
         budget.heartbeat()
     # one process per GPU: CUDA-tensor / RCCL IPC between processes needs the dmabuf IPC mode on
     # this ROCm (the legacy handle path fails with hipIpcGetMemHandle: invalid argument); set before

@@ -133,12 +133,17 @@ def test_relay_passes_a_termination_on_to_the_ranks(tmp_path):
 def test_bench_without_launcher_starts_the_ranks_itself():
     """`python bench.py --gpus 2` with no WORLD_SIZE: bench.py runs torch.distributed.run itself as
     a child. Here (no GPU) the two ranks fail at their first GPU call, and that failure is the
-    command's exit code, with no JSON line on stdout."""
+    command's exit code; the only line on stdout is rank 0's line so far: no value, truncated by
+    the error."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
     assert r.returncode != 0
-    assert r.stdout.strip() == ""
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) <= 1
+    if lines:
+        d = json.loads(lines[0])
+        assert d["value"] is None and d["truncated"] is True and d["truncated_by"] == "error", d
     assert "torch.distributed" in r.stderr or "ChildFailedError" in r.stderr or "rank" in r.stderr.lower()
 
 
@@ -420,3 +425,34 @@ def test_section_estimates_grow_with_the_work():
         ref_rows, cpu_sample_bytes, cpu_seconds = 1024, 2.2e9, 12.0
     small = bench.est_cpu_baseline(A(), 16384, 16384)
     assert bench.est_cpu_baseline(A(), 16384, 16384, big_rows=8192) > small > 24
+
+
+def test_e2e_memory_gate_follows_the_measured_memory(monkeypatch):
+    """configs[].end_to_end runs wherever the host copy of A fits the memory measured at that
+    moment (and the cap, less this process's RSS), 8 GiB + 5 % to spare; otherwise it says why."""
+    monkeypatch.setattr(bench, "host_mem_free", lambda: 300 << 30)
+    monkeypatch.setattr(bench, "process_rss", lambda: 2 << 30)
+    ok, mem = bench.e2e_memory_fit(131072, 131072, False, 0, cap=250 << 30)  # config 4: 137 GB
+    assert ok and mem["need_bytes"] == 8 * 131072 ** 2 and mem["host_free_bytes"] == 248 << 30
+    ok, mem = bench.e2e_memory_fit(131072, 131072, False, 0, cap=140 << 30)
+    assert not ok and mem["host_free_bytes"] == 138 << 30
+    monkeypatch.setattr(bench, "host_mem_free", lambda: 100 << 30)
+    assert bench.e2e_memory_fit(65536, 65536, False, 0)[0]  # config 3: 34 GB
+    assert not bench.e2e_memory_fit(131072, 131072, False, 0)[0]
+
+
+def test_an_uncaught_error_still_writes_the_line_so_far(tmp_path):
+    """A section error that ends the run (fatal at N > 1) leaves the line so far, truncated,
+    with the error, and the process fails."""
+    child = tmp_path / "rank0.py"
+    child.write_text(f"import sys\nsys.path.insert(0, {REPO!r})\nimport bench\n"
+                     "b = bench.Budget(1e6)\nr = bench.Report(sys.stdout, b)\n"
+                     "r.update({'metric': bench.METRIC, 'value': 42.0})\nr.on_uncaught()\n"
+                     "def boom():\n    raise MemoryError('hipHostRegister: out of memory')\n"
+                     "b.run('config 4 end_to_end', 0.0, boom)\n")
+    p = subprocess.run([sys.executable, str(child)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and "MemoryError" in p.stderr
+    (line,) = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    d = json.loads(line)
+    assert d["value"] == 42.0 and d["truncated"] is True and d["truncated_by"] == "error"
+    assert d["truncated_in"] == "config 4 end_to_end" and d["error"].startswith("MemoryError")
