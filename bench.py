@@ -644,8 +644,8 @@ def main():
 
 # ---- section time estimates (s) for the budget: generous upper bounds from the round-4/5 box
 # records (sections_s of profiles/r05 bench lines); a section runs only if its estimate fits
-GEN_GBPS = 6.0     # host synthetic fill + first touch (16 threads)
-PIN_GBPS = 15.0    # hipHostRegister of a host matrix
+GEN_GBPS = 20.0    # host synthetic fill + first touch (16 threads; r05: 137 GB filled, pinned and
+PIN_GBPS = 40.0    #   distributed 3 times in 10 s) / hipHostRegister of a host matrix
 H2D_GBPS = 40.0    # per-GPU host -> device distribution (56 measured: 0.7 of it)
 REF_TEXT_GBPS = 0.08  # the reference's fscanf load of its text input, per byte of A (with the file write)
 
@@ -674,9 +674,11 @@ def est_ref_run(nbytes, P):
     return 3.0 + nbytes / (REF_TEXT_GBPS * 1e9) / 10 + 100 * nbytes / rate
 
 
-def est_cpu_baseline(args, R, C, ref_rows=None, big_rows=None, sweep=True, port_bytes=None):
+def est_cpu_baseline(args, R, C, ref_rows=None, big_rows=None, sweep=True, port_bytes=None, cpu_seconds=None):
     port_bytes = min(8 * R * C, args.cpu_sample_bytes if port_bytes is None else port_bytes)
-    t = 3.0 + port_bytes / (GEN_GBPS * 1e9) + 2 * args.cpu_seconds
+    cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
+    # inputs generated, the first timed iteration, then about cpu_seconds of iterations
+    t = 3.0 + port_bytes / (6e9) + port_bytes / 4e9 + 2 * cpu_seconds
     small = 8 * min(R, ref_rows or args.ref_rows) * C
     t += 2 * est_ref_run(small, 16)
     if sweep:
@@ -1121,7 +1123,8 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
             ref_rows = min(R, max(128, int(args.config_ref_bytes // (8 * C))))
             entry["cpu_baseline"] = budget.run(
                 f"{name} cpu_baseline",
-                est_cpu_baseline(args, R, C, ref_rows=ref_rows, sweep=False, port_bytes=args.config_cpu_sample_bytes),
+                est_cpu_baseline(args, R, C, ref_rows=ref_rows, sweep=False, port_bytes=args.config_cpu_sample_bytes,
+                                 cpu_seconds=args.config_cpu_seconds),
                 guarded, cpu_baseline, args, alg, R, C, y, None, ref_rows, args.config_cpu_sample_bytes,
                 args.config_cpu_seconds, ("spread",), (), None, collective=False)
     return entry
@@ -1508,7 +1511,10 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
            **({"exact_vs_reference": bool(np.array_equal(y_exact[:rows], r["y"]))}
               if y_exact is not None and alg == "rowwise" else {})}
     l3 = (cache or {}).get("l3_bytes")
+    l3s = (cache or {}).get("l3_bytes_system")
+    # the sample against the L3 of the CPUs the ranks run on, and against the host's whole L3
     out["sample_over_l3"] = round(nbytes / l3, 2) if l3 else None
+    out["sample_over_l3_system"] = round(nbytes / l3s, 2) if l3s else None
     if big_rows:
         brows = splittable_rows(alg, min(R, big_rows), P)
         if brows <= rows:
@@ -1534,6 +1540,7 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
                     pt["efficiency"] = round(t1 / pt["s_per_iter"] / pt["P"], 3) if t1 else None
                 out.update(value=round(bbytes / rb["seconds"] / 1e9, 3), ms_per_step=round(rb["seconds"] * 1e3, 3),
                            sample=sample_text(brows, rb, relb), sample_over_l3=round(bbytes / l3, 2) if l3 else None,
+                           sample_over_l3_system=round(bbytes / l3s, 2) if l3s else None,
                            sweep_beyond_cache={"points": pts, "semantics": "the same executable on the beyond-cache "
                                                "sample; S = T1/TP, E = S/P (README.md:47-50)"},
                            small_sample=small)

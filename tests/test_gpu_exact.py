@@ -405,13 +405,18 @@ def test_engine_exact_panels_fill_synth_and_toggle(comm1):
 
 
 def _hip_runtime():
-    """The HIP runtime this process already has loaded (the library's), through ctypes."""
+    """The HIP runtime libmatvec_gpu.so is linked against, through ctypes. A process may hold two
+    (PyTorch's wheel ships its own libamdhip64, with its own per-thread error state), so the one
+    to use is the library's own dependency as the loader resolves it (ldd), which is already
+    mapped."""
     import ctypes
+    import subprocess
 
-    for line in open("/proc/self/maps"):
-        if "libamdhip64.so" in line:
-            return ctypes.CDLL(line.split()[-1])
-    raise AssertionError("libamdhip64 is not loaded")
+    out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    path = next(ln.split("=>")[1].split("(")[0].strip() for ln in out.splitlines() if "libamdhip64" in ln)
+    mapped = {os.path.realpath(ln.split()[-1]) for ln in open("/proc/self/maps") if "libamdhip64" in ln}
+    assert os.path.realpath(path) in mapped, (path, mapped)
+    return ctypes.CDLL(path)
 
 
 @pytest.fixture
