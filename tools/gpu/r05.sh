@@ -45,6 +45,13 @@ for step in $STEPS; do
         > $OUT/pmc_cfg2.log 2>&1; rc=$?
     tail -3 $OUT/pmc_cfg2.log; [ $rc -eq 0 ] || exit $rc
     python3 tools/pmc_traffic.py --outdir $OUT/pmc_summary --M 16384 --K 16384 $OUT/pmc/cfg2 ;;
+  evprobe)
+    echo "== event timing probe (untraced, then under the kernel trace)"
+    timeout -k 10 120 python3 tools/probes/event_timing_probe.py 16384 16384 50 > $OUT/event_probe.jsonl 2> $OUT/event_probe.err; rc=$?
+    cat $OUT/event_probe.jsonl; [ $rc -eq 0 ] || exit $rc
+    cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/evprof -o run -- \
+        python3 $ROOT/tools/probes/event_timing_probe.py 16384 16384 50 > $ROOT/$OUT/event_probe_traced.jsonl 2>> $ROOT/$OUT/event_probe.err; rc=$?
+    cd $ROOT; cat $OUT/event_probe_traced.jsonl; [ $rc -eq 0 ] || exit $rc ;;
   rehearse8)
     echo "== N=8 same-device rehearsal with a 150 s budget"
     MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 150 \
