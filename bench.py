@@ -127,10 +127,13 @@ class Budget:
     not fit returns a skip marker instead. `current` names the section in progress (a truncated
     line says where the run was)."""
 
-    def __init__(self, limit_s: float, distributed: bool = False, device=None):
+    def __init__(self, limit_s: float, distributed: bool = False, device=None, verbose: bool = True,
+                 reserve_s: float = 0.0):
         self.limit_s = float(limit_s)
         self.distributed = distributed
         self.device = device
+        self.verbose = verbose      # section log lines (rank 0 only at N > 1)
+        self.reserve_s = reserve_s  # kept back for the teardown and the line
         self.sections: dict[str, float] = {}
         self.skipped: list[str] = []
         self.current: str | None = None
@@ -143,7 +146,7 @@ class Budget:
         return self.limit_s - self.used()
 
     def fits(self, need_s: float, collective: bool = True) -> bool:
-        ok = self.left() >= need_s
+        ok = self.left() - self.reserve_s >= need_s
         if self.distributed and collective:
             import torch
             import torch.distributed as dist
@@ -159,11 +162,13 @@ class Budget:
     def run(self, name: str, need_s: float, fn, *a, collective: bool = True):
         if not self.fits(need_s, collective):
             self.skipped.append(name)
-            log(f"bench: section {name} skipped: needs ~{need_s:.0f} s, {self.left():.0f} s of the budget left")
+            if self.verbose:
+                log(f"bench: section {name} skipped: needs ~{need_s:.0f} s, {self.left():.0f} s of the budget left")
             return self.marker(need_s)
         t0, prev = time.perf_counter(), self.current
         self.current = name
-        log(f"bench: [{self.used():.0f} s] section {name} (estimate {need_s:.0f} s)")
+        if self.verbose:
+            log(f"bench: [{self.used():.0f} s] section {name} (estimate {need_s:.0f} s)")
         try:
             return fn(*a)
         except BaseException:
@@ -171,7 +176,8 @@ class Budget:
             raise
         finally:
             self.sections[name] = round(time.perf_counter() - t0, 2)
-            log(f"bench: [{self.used():.0f} s] section {name} done in {self.sections[name]:.1f} s")
+            if self.verbose:
+                log(f"bench: [{self.used():.0f} s] section {name} done in {self.sections[name]:.1f} s")
             self.current = prev
 
     def heartbeat(self, every_s: float = 30.0) -> None:
@@ -186,7 +192,8 @@ class Budget:
         threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
 
     def record(self) -> dict:
-        return {"limit_s": self.limit_s, "used_s": round(self.used(), 1), "skipped": list(self.skipped)}
+        return {"limit_s": self.limit_s, "reserve_s": self.reserve_s, "used_s": round(self.used(), 1),
+                "skipped": list(self.skipped)}
 
 
 class Report:
@@ -401,7 +408,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     n = args.gpus
-    budget = Budget(args.budget_s)
+    budget = Budget(args.budget_s, verbose=rank == 0, reserve_s=10.0)
     report = Report(json_out, budget)
     if rank == 0:
         # from here on a time limit still gets a line: the fields known so far, "truncated": true
@@ -589,7 +596,7 @@ def main():
     # end-to-end: root's host A -> shards -> multiply -> y on the root
     if not args.no_e2e and args.e2e_iters > 0:
         e2e = section("end_to_end", est_e2e(total_bytes, n, args.e2e_iters, distributed), end_to_end, args, eng, mm,
-                      R, C, rank, distributed, barrier, y, total_bytes, local)
+                      R, C, rank, distributed, barrier, y, total_bytes, local, budget)
         if rank == 0:
             report["end_to_end"] = e2e
 
@@ -629,8 +636,11 @@ def main():
         if n > 1:
             # the executables' one-process-drives-N-GPUs path (ncclCommInitAll, grouped exchange),
             # which the rank-per-GPU sections above never run; the other ranks have exited
-            sp = budget.run("single_process", est_single_process(R, C, n), single_process_section, args, n, R, C,
-                            caller_nccl, None, budget, collective=False)
+            if single_process_blocker(n):  # nothing to run here: record why, whatever the budget
+                sp = single_process_section(args, n, R, C, caller_nccl, None, budget)
+            else:
+                sp = budget.run("single_process", est_single_process(R, C, n), single_process_section, args, n, R,
+                                C, caller_nccl, None, budget, collective=False)
             report["single_process"] = sp
             if isinstance(sp, dict) and sp.get("error"):
                 WARNINGS.append(f"single_process: the MVG_NGPUS={n} executable failed (rc {sp.get('rc')}): "
@@ -721,6 +731,17 @@ def warm(e, min_launches, distributed, local, seconds=0.1):
     e.sync()
 
 
+def single_process_blocker(n):
+    """Why this box cannot run the one-process-drives-N-GPUs form (None when it can)."""
+    import torch
+
+    have = torch.cuda.device_count()
+    if have < n or os.environ.get("MVG_SAME_DEVICE") == "1":
+        return (f"needs {n} devices in one process, {have} visible"
+                + (" (MVG_SAME_DEVICE rehearsal: every rank on one GPU)" if os.environ.get("MVG_SAME_DEVICE") == "1" else ""))
+    return None
+
+
 def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=None):
     """The drop-in executables' single-process form of the same workload: ONE process drives all
     N GPUs (mvg_comm_init_all -> ncclCommInitAll over N devices, the grouped ncclCommSplit and the
@@ -736,12 +757,9 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
     import subprocess
     import tempfile
 
-    import torch
-
-    have = torch.cuda.device_count()
-    if have < n or os.environ.get("MVG_SAME_DEVICE") == "1":
-        return {"ran": False, "why": f"needs {n} devices in one process, {have} visible"
-                + (" (MVG_SAME_DEVICE rehearsal: every rank on one GPU)" if os.environ.get("MVG_SAME_DEVICE") == "1" else "")}
+    why = single_process_blocker(n)
+    if why:
+        return {"ran": False, "why": why}
     exe = exe or os.path.join(REPO, "bin", f"multiplier_{args.alg}")
     if not os.access(exe, os.X_OK):
         return {"ran": False, "why": f"{os.path.relpath(exe, REPO)} not built"}
@@ -1078,7 +1096,7 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
                 e2e = {"skipped": "memory", **mem}
             else:
                 e2e = budget.run(f"{name} end_to_end", est_e2e(total, n, args.e2e_iters, distributed), guarded,
-                                 end_to_end, args, e, mm, R, C, rank, distributed, barrier, y, total, local)
+                                 end_to_end, args, e, mm, R, C, rank, distributed, barrier, y, total, local, budget)
                 if isinstance(e2e, dict):
                     e2e["host_memory"] = mem
         if not args.no_exact:
@@ -1299,7 +1317,7 @@ def rccl_report(path, distributed, rank):
             "links": {k: sorted(v) for k, v in sorted(links.items())}, "log_samples": samples}
 
 
-def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_bytes, local):
+def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_bytes, local, budget=None):
     """The reference's timing semantics on the GPU path: A and x preloaded in the root's host
     memory; each iteration distributes them, multiplies, and ends when the root holds y (max over
     ranks). Two distributions:
@@ -1307,7 +1325,11 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
                   shard over its own PCIe link, all at once (MPICH's shared-memory scatter analog;
                   N = 1: one process, plain pinned memory).
       root_send : only the root touches A; it stages each peer's shard through its GPU and
-                  ncclSends it over xGMI (the reference's sequential root sends). N > 1 only."""
+                  ncclSends it over xGMI (the reference's sequential root sends). N > 1 only.
+    With a `budget`, an iteration after the first runs only if 1.5x the slowest one so far still
+    fits (all-reduced), and root_send only if (N - 1)x the shared form's iteration does — the
+    root pushes N - 1 shards through its one link — so a slow transport (the same-device
+    rehearsal's sockets) costs at most one iteration beyond the budget; `iters` says how many ran."""
     import torch
     import torch.distributed as dist
 
@@ -1315,7 +1337,9 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
 
     def timed(fn):
         times = []
-        for _ in range(args.e2e_iters):
+        for it in range(args.e2e_iters):
+            if it > 0 and budget is not None and not budget.fits(1.5 * max(times)):
+                break
             barrier()
             ts = time.perf_counter()
             y = fn()
@@ -1326,9 +1350,12 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
             times.append(float(tt[0]))
         if rank == 0:
             expect(np.array_equal(y, y_ref), "end-to-end y differs from the device-resident y")
-        return {"mean_s": float(np.mean(times)), "iters": len(times),
-                "GBps": total_bytes / float(np.mean(times)) / 1e9,
-                "gflops": 2 * R * C / float(np.mean(times)) / 1e9}
+        out_t = {"mean_s": float(np.mean(times)), "iters": len(times),
+                 "GBps": total_bytes / float(np.mean(times)) / 1e9,
+                 "gflops": 2 * R * C / float(np.mean(times)) / 1e9}
+        if len(times) < args.e2e_iters:
+            out_t["stopped"] = "budget"
+        return out_t
 
     out = {"semantics": "reference: root holds A, x in host memory; distribute + multiply + y on root"}
     from matvec_mpi_multiplier_amd.hostshare import SharedHostMatrix, shm_free_bytes
@@ -1364,9 +1391,14 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
         out["shared"]["distribution"] = ("per-GPU H2D from " + ("shared " if distributed else "")
                                          + ("pinned" if pinned else "pageable") + " host memory")
     if distributed:
-        out["root_send"] = timed(lambda: (eng.distribute(A if rank == 0 else None, x), eng.multiply(),
-                                          eng.collect())[2])
-        out["root_send"]["distribution"] = "root H2D staging + ncclSend over xGMI"
+        per = out["shared"]["mean_s"] if isinstance(out.get("shared"), dict) else 8 * R * C / 20e9
+        need = 1.5 * max(1, n_ranks(distributed) - 1) * per
+        if budget is not None and not budget.fits(need):
+            out["root_send"] = budget.marker(need)
+        else:
+            out["root_send"] = timed(lambda: (eng.distribute(A if rank == 0 else None, x), eng.multiply(),
+                                              eng.collect())[2])
+            out["root_send"]["distribution"] = "root H2D staging + ncclSend over xGMI"
     if pinned:
         _l.mvg_host_unregister(reg[0])
     if shared is not None:

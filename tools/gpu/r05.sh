@@ -53,9 +53,15 @@ for step in $STEPS; do
         python3 $ROOT/tools/probes/event_timing_probe.py 16384 16384 50 > $ROOT/$OUT/event_probe_traced.jsonl 2>> $ROOT/$OUT/event_probe.err; rc=$?
     cd $ROOT; cat $OUT/event_probe_traced.jsonl; [ $rc -eq 0 ] || exit $rc ;;
   rehearse8)
-    echo "== N=8 same-device rehearsal with a 150 s budget"
-    MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 150 \
+    echo "== N=8 same-device rehearsal with a 120 s budget (the launcher-free form: bench.py starts the ranks)"
+    MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 120 \
         > $OUT/bench_n8.json 2> $OUT/bench_n8.err; rc=$?
-    tail -c 400 $OUT/bench_n8.json; tail -3 $OUT/bench_n8.err; ok $rc || exit $rc ;;
+    tail -c 400 $OUT/bench_n8.json; grep "bench:" $OUT/bench_n8.err | tail -5; ok $rc || exit $rc ;;
+  sigterm8)
+    echo "== N=8 same-device run terminated by a time limit mid-run: the line so far must come out (last step)"
+    MVG_SAME_DEVICE=1 timeout -s TERM -k 60 75 python3 bench.py --gpus 8 --steps 5 --warmup 2 \
+        > $OUT/bench_n8_sigterm.json 2> $OUT/bench_n8_sigterm.err; rc=$?
+    echo "rc=$rc"; tail -c 600 $OUT/bench_n8_sigterm.json; grep "bench:" $OUT/bench_n8_sigterm.err | tail -5
+    exit 0 ;;
   esac
 done
