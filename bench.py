@@ -1409,7 +1409,7 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
     # (per-GPU rate of the slowest rank against the link's spec and a plain pinned H2D copy)
     link = pcie_roofline(local)
     if link is not None:
-        best = min((v["mean_s"] for v in (out.get("shared"), out.get("root_send")) if isinstance(v, dict)),
+        best = min((v["mean_s"] for v in (out.get("shared"), out.get("root_send")) if isinstance(v, dict) and "mean_s" in v),
                    default=None)
         if best is not None:
             per_gpu = total_bytes / n_ranks(distributed) / best / 1e9

@@ -342,3 +342,43 @@ def test_mpiexec_exact_colwise_mpich_reduce_order(tmp_path, golden, P):
                MVG_Y_OUT=yout)
     assert r.returncode == 0, r.stderr[-2000:]
     assert yout.read_text() == "".join("%.17g\n" % v for v in golden[f"sq_720/colwise/P{P}"])
+
+
+@pytest.mark.gpu
+def test_bench_sigterm_mid_run_keeps_the_line(tmp_path):
+    """The driver's N = 1 command terminated by a time limit while a GPU section runs: rank 0's
+    watcher writes the line so far (headline included, `truncated`, the section it was in) and
+    the process exits 128 + SIGTERM; sections that finished are in the line."""
+    import json
+    import signal
+    import threading
+
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "2",
+                          "--no-cpu-baseline", "--configs", "3,4", "--config-e2e", "4"],
+                         cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    seen = threading.Event()
+    err = []
+
+    def watch():
+        for ln in p.stderr:
+            err.append(ln)
+            if "section config 4 end_to_end (estimate" in ln:
+                seen.set()
+
+    t = threading.Thread(target=watch, daemon=True)
+    t.start()
+    try:
+        assert seen.wait(timeout=100), "".join(err[-20:])
+        p.send_signal(signal.SIGTERM)
+        out = p.stdout.read()
+        assert p.wait(timeout=60) == 128 + signal.SIGTERM
+    finally:
+        if p.poll() is None:
+            p.kill()
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["truncated"] is True and d["truncated_by"] == "SIGTERM" and d["truncated_in"] == "config 4 end_to_end"
+    assert d["value"] > 0 and d["roofline"]["frac"] > 0 and d["exact"]["value"] > 0
+    assert [c["config"] for c in d["configs"]] == ["config 3"]  # config 4 had not finished
+    assert "headline" in d["sections_s"] and "config 3" in d["sections_s"]
