@@ -1,7 +1,12 @@
 """How the engine's HIP-event kernel timing compares with back-to-back wall time for the tree
 and the row-major exact GEMV at config 2 (development probe; one JSON line per form).
 
-    python tools/probes/event_timing_probe.py [M] [K] [steps]
+    python tools/probes/event_timing_probe.py [M] [K] [steps] [forms] [torch]
+
+forms: "tree,exact" (default) or one of them. torch: what PyTorch does in the process before the
+engine exists — "none" (not imported), "sync" (the bench's torch.cuda.set_device +
+torch.cuda.synchronize: PyTorch's own HIP runtime comes up on the device) or "ops" (also a
+device tensor, a page-locked host tensor and a copy on a side stream, as the bench's PCIe probe).
 
 For each form: a warm-up, then `steps` multiplies timed by events on every launch
 (kernel_timing(1)), the same with every 5th launch (the bench's setting), and 3 * steps
@@ -21,18 +26,32 @@ def main():
     M = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    forms = (sys.argv[4] if len(sys.argv) > 4 else "tree,exact").split(",")
+    mode = sys.argv[5] if len(sys.argv) > 5 else "none"
+    if mode != "none":
+        import torch
+
+        torch.cuda.set_device(0)
+        torch.cuda.synchronize()
+        if mode == "ops":
+            d = torch.ones(1 << 20, dtype=torch.float64, device="cuda:0")
+            h = torch.empty(1 << 20, dtype=torch.float64, pin_memory=True)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                d.copy_(h, non_blocking=True)
+            torch.cuda.synchronize()
     os.environ["MVG_NO_PANELS"] = "1"  # the exact form a fresh distribution runs (row-major)
     comm = mm.Comm.init_all([0])
     eng = mm.Multiplier("rowwise", M, K, comm)
     eng.fill_synth()
     nbytes = 8 * (M * K + K + M)
     try:
-        for form in ("tree", "exact"):
+        for form in forms:
             eng.set_exact(form == "exact")
             for _ in range(300):
                 eng.multiply()
             eng.sync()
-            out = {"form": form, "M": M, "K": K, "steps": steps}
+            out = {"form": form, "torch": mode, "M": M, "K": K, "steps": steps}
             for every in (1, 5):
                 eng.kernel_timing(every)
                 for _ in range(steps):
