@@ -173,12 +173,29 @@ SIGNATURES = {
 }
 
 
+def _torch_first() -> None:
+    """PyTorch's ROCm wheel bundles its own HIP and HSA runtimes. Two HSA runtimes in one process
+    cannot both open the GPU: whichever initialises second finds "no ROCm-capable device"
+    (profiles/r05/torch_order/). With PyTorch's libraries loaded first, this library's HIP runtime
+    binds to PyTorch's HSA runtime through the global symbol scope, and the two HIP runtimes then
+    share the device in any order of use (with the tree kernel's time unchanged). So when PyTorch
+    is installed it is imported before the library is loaded; MVG_NO_TORCH=1 skips that (a
+    process that never uses PyTorch's GPU side)."""
+    if os.environ.get("MVG_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: the HIP library is required (no CPU fallback). "
             "Build it with `make -C <repo>` or `python -c 'import __graft_entry__ as g; g.build()'`."
         )
+    _torch_first()
     lib = C.CDLL(LIB_PATH)  # RTLD_LOCAL: a global RCCL ahead of torch's double-frees at exit
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import case_inputs, golden_runs, max_rel
+from conftest import REPO as REPO_ROOT, case_inputs, golden_runs, max_rel
 from matvec_mpi_multiplier_amd import _lib
 from matvec_mpi_multiplier_amd import multiplier as mm
 from oracle import oracle
@@ -601,3 +601,27 @@ def test_overlapped_distribution_gives_the_same_y(comm1, alg, chunks):
                 assert np.array_equal(y, want), (alg, chunks)
             else:
                 assert max_rel(y, want) <= TOL, (alg, chunks)
+
+
+@pytest.mark.gpu
+def test_library_and_pytorch_share_the_device_in_any_order():
+    """PyTorch's wheel bundles its own HIP + HSA runtimes; two HSA runtimes in one process cannot
+    both open the GPU (profiles/r05/torch_order/library_first.err). The package imports PyTorch
+    before loading the library, so both runtimes work whichever touches the device first."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, {repo!r})\n"
+            "from matvec_mpi_multiplier_amd import multiplier as mm\n"
+            "import numpy as np, torch\n"
+            "{first}\n"
+            "A = np.arange(64 * 48, dtype=np.float64).reshape(64, 48) / 7; x = np.linspace(0, 1, 48)\n"
+            "y = mm.multiply_std_rowwise(A, x)\n"
+            "{second}\n"
+            "assert np.allclose(y, A @ x, rtol=1e-13, atol=0)\n"
+            "print('ok', float(t.sum()))\n")
+    torch_op = "torch.cuda.set_device(0); t = torch.ones(1000, device='cuda:0', dtype=torch.float64); torch.cuda.synchronize()"
+    for first, second in ((torch_op, ""), ("", torch_op)):
+        r = subprocess.run([sys.executable, "-c", code.format(repo=REPO_ROOT, first=first, second=second)],
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0 and r.stdout.startswith("ok 1000.0"), r.stderr[-2000:]

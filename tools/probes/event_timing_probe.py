@@ -4,9 +4,11 @@ and the row-major exact GEMV at config 2 (development probe; one JSON line per f
     python tools/probes/event_timing_probe.py [M] [K] [steps] [forms] [torch]
 
 forms: "tree,exact" (default) or one of them. torch: what PyTorch does in the process before the
-engine exists — "none" (not imported), "sync" (the bench's torch.cuda.set_device +
-torch.cuda.synchronize: PyTorch's own HIP runtime comes up on the device) or "ops" (also a
-device tensor, a page-locked host tensor and a copy on a side stream, as the bench's PCIe probe).
+engine exists — "none" (its GPU side unused; the package imports it before loading the library
+since round 5, MVG_NO_TORCH=1 keeps it out), "set" (torch.cuda.set_device), "sync" (also
+torch.cuda.synchronize: PyTorch's own HIP runtime — a second one, with its own HSA runtime, in
+the wheel — comes up on the device), "ops" (also a device tensor, a page-locked host tensor and
+a copy on a side stream, as the bench's PCIe probe); "late": set + sync after the engine exists.
 
 For each form: a warm-up, then `steps` multiplies timed by events on every launch
 (kernel_timing(1)), the same with every 5th launch (the bench's setting), and 3 * steps
@@ -19,6 +21,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+if os.environ.get("PROBE_TORCH_FIRST") == "1":  # PyTorch's libraries loaded before the library's
+    import torch  # noqa: F401
 from matvec_mpi_multiplier_amd import multiplier as mm  # noqa: E402
 
 
@@ -28,11 +32,12 @@ def main():
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
     forms = (sys.argv[4] if len(sys.argv) > 4 else "tree,exact").split(",")
     mode = sys.argv[5] if len(sys.argv) > 5 else "none"
-    if mode != "none":
+    if mode not in ("none", "late"):
         import torch
 
         torch.cuda.set_device(0)
-        torch.cuda.synchronize()
+        if mode != "set":
+            torch.cuda.synchronize()
         if mode == "ops":
             d = torch.ones(1 << 20, dtype=torch.float64, device="cuda:0")
             h = torch.empty(1 << 20, dtype=torch.float64, pin_memory=True)
@@ -44,6 +49,11 @@ def main():
     comm = mm.Comm.init_all([0])
     eng = mm.Multiplier("rowwise", M, K, comm)
     eng.fill_synth()
+    if mode == "late":  # PyTorch's runtime comes up after the library's (the bench's order)
+        import torch
+
+        torch.cuda.set_device(0)
+        torch.cuda.synchronize()
     nbytes = 8 * (M * K + K + M)
     try:
         for form in forms:
