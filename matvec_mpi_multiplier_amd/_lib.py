@@ -174,13 +174,14 @@ SIGNATURES = {
 
 
 def _torch_first() -> None:
-    """PyTorch's ROCm wheel bundles its own HIP and HSA runtimes. Two HSA runtimes in one process
-    cannot both open the GPU: whichever initialises second finds "no ROCm-capable device"
-    (profiles/r05/torch_order/). With PyTorch's libraries loaded first, this library's HIP runtime
-    binds to PyTorch's HSA runtime through the global symbol scope, and the two HIP runtimes then
-    share the device in any order of use (with the tree kernel's time unchanged). So when PyTorch
-    is installed it is imported before the library is loaded; MVG_NO_TORCH=1 skips that (a
-    process that never uses PyTorch's GPU side)."""
+    """PyTorch's ROCm wheel bundles its own HIP and HSA runtimes (libamdhip64.so, soname
+    libamdhip64.so.7, HIP 7.0). Loaded after this library, they make a second HIP + HSA runtime
+    in the process, and two HSA runtimes cannot both open the GPU: whichever initialises second
+    finds "no ROCm-capable device" (profiles/r05/torch_order/). Loaded first, PyTorch's copy
+    satisfies this library's dependency on libamdhip64.so.7 (same soname), so the process has one
+    HIP runtime that both use, in any order, with the tree kernel's time unchanged. So when
+    PyTorch is installed it is imported before the library is loaded; MVG_NO_TORCH=1 skips that
+    (a process that never uses PyTorch's GPU side then runs on /opt/rocm's runtime)."""
     if os.environ.get("MVG_NO_TORCH") == "1":
         return
     try:

@@ -405,16 +405,18 @@ def test_engine_exact_panels_fill_synth_and_toggle(comm1):
 
 
 def _hip_runtime():
-    """The HIP runtime libmatvec_gpu.so is linked against, through ctypes. A process may hold two
-    (PyTorch's wheel ships its own libamdhip64, with its own per-thread error state), so the one
-    to use is the library's own dependency as the loader resolves it (ldd), which is already
-    mapped."""
+    """The HIP runtime libmatvec_gpu.so runs on, through ctypes. PyTorch's wheel ships its own
+    libamdhip64 with the same soname (libamdhip64.so.7); the package loads PyTorch first, so the
+    library's dependency resolves to that copy and the process maps one HIP runtime. Without
+    PyTorch (MVG_NO_TORCH=1) it is the loader's resolution of the library's own dependency."""
     import ctypes
     import subprocess
 
+    mapped = {os.path.realpath(ln.split()[-1]) for ln in open("/proc/self/maps") if "libamdhip64" in ln}
+    if len(mapped) == 1:
+        return ctypes.CDLL(mapped.pop())
     out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
     path = next(ln.split("=>")[1].split("(")[0].strip() for ln in out.splitlines() if "libamdhip64" in ln)
-    mapped = {os.path.realpath(ln.split()[-1]) for ln in open("/proc/self/maps") if "libamdhip64" in ln}
     assert os.path.realpath(path) in mapped, (path, mapped)
     return ctypes.CDLL(path)
 
