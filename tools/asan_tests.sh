@@ -22,7 +22,7 @@ cd "$REPO"
 # ranks started by mpiexec inside the tests (the real reference, oracle/_ref) are not ours:
 # they get neither the runtime nor the sanitized libraries
 set +e
-env MVG_LIB="$REPO/build/asan/libmatvec_gpu.so" MVG_ORACLE_LIB="$REPO/build/asan/liboracle.so" \
+env MVG_LIB="$REPO/build/asan/libmatvec_gpu.so" MVG_ORACLE_LIB="$REPO/build/asan/liboracle.so" MVG_NO_TORCH=1 \
     ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1:detect_odr_violation=0" \
     UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1" \
     LD_PRELOAD="$RT" \
