@@ -11,7 +11,8 @@ to rank 0). K steps are timed between barrier + device synchronize on both sides
 is the max over ranks; value = algorithmic bytes of all ranks / that time.
 
 Also reported: `roofline` (the GEMV kernel alone: bytes per launch / its mean duration from
-HIP events on the engine stream; peak 8 TB/s; `traffic` from the committed rocprofv3 PMC
+HIP events on the engine stream — at one rank one event pair spanning the timed GEMVs, at N > 1
+every 5th step's GEMV bracketed; peak 8 TB/s; `traffic` from the committed rocprofv3 PMC
 summary when one matches this configuration), `cpu_baseline` (rank 0 at N = 1: the real
 reference, oracle/_ref under mpiexec, on a sample of the same matrix, with the oracle's
 restatement of its MPI loop on the full matrix beside it; the restatement alone when the
@@ -69,8 +70,11 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
     ap.add_argument("--cols", type=int, default=SHARD)
     ap.add_argument("--e2e-iters", type=int, default=3)
-    ap.add_argument("--event-every", type=int, default=5,
-                    help="bracket every Nth step's GEMV with HIP events (kernel duration for the roofline)")
+    ap.add_argument("--event-every", type=int, default=None,
+                    help="kernel duration for the roofline: bracket every Nth step's GEMV with HIP events "
+                         "(N > 0), or -1: one event pair spanning the timed steps' GEMVs (default -1 at one "
+                         "rank: no marker between the steps; 5 at N > 1, where the GEMV stream also waits "
+                         "on the exchange)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=None)
@@ -456,6 +460,8 @@ def main():
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     budget.distributed, budget.device = distributed, f"cuda:{local}"
+    if args.event_every is None:
+        args.event_every = 5 if distributed else -1
 
     def barrier():
         if distributed:

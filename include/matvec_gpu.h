@@ -307,7 +307,11 @@ int mvg_engine_collect(mvg_engine* e, double* y_host);
 int mvg_engine_stream(const mvg_engine* e, int local_index, void** stream);
 /* Average GEMV kernel time (ms) over the multiply calls since the last reset, measured with
  * hipEvents bracketing the kernel on each local device's stream (max over local devices).
- * every = N > 0 brackets every Nth multiply call (1 = all); 0 turns timing off. */
+ * every = N > 0 brackets every Nth multiply call (1 = all); 0 turns timing off; -1 times spans:
+ * one event before the first GEMV after a reset or a sync and one at the next mvg_engine_sync,
+ * nothing between the GEMVs of the span (a bracketing marker stalls the stream around its
+ * kernel), so the average is the span over its multiplies (the GEMVs back to back, with their
+ * dispatch gaps; at more than one rank it also holds the GEMV stream's waits on the exchange). */
 int mvg_engine_kernel_timing(mvg_engine* e, int every);
 int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches);
 int mvg_engine_destroy(mvg_engine* e);

@@ -103,6 +103,7 @@ struct Shard {
     size_t stage_elems = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
+    hipEvent_t span_t0 = nullptr, span_t1 = nullptr;  // span timing (mvg_engine_kernel_timing(-1))
 };
 
 }  // namespace
@@ -116,7 +117,9 @@ struct mvg_engine {
     bool distributed = false;
     bool exact = false;         // bit-exact mode: mvg_gemv_exact + the reference's combine orders
     int overlap_chunks = 0;     // > 1: distribute in row chunks, each chunk's GEMV behind its copy
-    int timing_every = 0;       // record kernel events on every Nth multiply (0 = off)
+    int timing_every = 0;       // record kernel events on every Nth multiply (0 = off, -1 = span)
+    int64_t span_multiplies = 0;  // span timing: multiplies since the span's first event (0 = none open)
+    bool span_valid = true;       // no chunked distribution's copies inside the open span
     int64_t nx = 0;             // multiplies with an exchange issued so far
     bool x_pending = false;     // an exchange may still run (slot (nx - 1) % ring)
     int ring = kRing;           // ring length in use (MVG_XRING, 1 = exchange on the GEMV stream)
@@ -258,6 +261,8 @@ void free_shard(Shard& s) {
         (void)hipEventDestroy(ev.second);
     }
     for (hipEvent_t ev : s.chunk_ev) (void)hipEventDestroy(ev);
+    if (s.span_t0) (void)hipEventDestroy(s.span_t0);
+    if (s.span_t1) (void)hipEventDestroy(s.span_t1);
     if (s.copy_ready) (void)hipEventDestroy(s.copy_ready);
     s.ev_pool.clear();
     for (int k = 0; k < MVG_MAX_XSTEPS; ++k)
@@ -900,7 +905,9 @@ int mvg_engine_kernel_timing(mvg_engine* e, int enable) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
     int rc = mvg_engine_sync(e);
     if (rc != MVG_OK) return rc;
-    e->timing_every = enable > 0 ? enable : 0;
+    e->timing_every = enable > 0 ? enable : enable == -1 ? -1 : 0;
+    e->span_multiplies = 0;
+    e->span_valid = true;
     e->multiply_calls = 0;
     e->kernel_ms_sum = 0.0;
     e->kernel_launches = 0;
@@ -916,6 +923,14 @@ int mvg_engine_multiply(mvg_engine* e) {
     bool chunked = false;  // a chunked distribution is pending: the GEMVs wait on copies, not timed
     for (auto& s : e->shards) chunked |= s.chunks_pending;
     const bool timed = e->timing_every > 0 && (e->multiply_calls++ % e->timing_every) == 0 && !chunked;
+    // span timing: one event before the first GEMV of the span, one at the next sync, no marker
+    // between the GEMVs in between (a timing marker costs the stream ~6 us around the kernel it
+    // brackets, profiles/r05/t5c); a chunked distribution's copies inside the span void it
+    const bool span_open = e->timing_every == -1 && e->span_multiplies == 0 && !chunked;
+    if (e->timing_every == -1) {
+        if (chunked) e->span_valid = false;
+        ++e->span_multiplies;
+    }
     const bool serial = e->ring == 1;
     const int b = solo ? 0 : (int)(e->nx % e->ring);
     // The GEMV writes dy_parts[b]; the exchange that last read it was multiply nx - ring's. The
@@ -946,6 +961,11 @@ int mvg_engine_multiply(mvg_engine* e) {
         }
         const bool panels = e->exact && s.dAp && s.panels_fresh;
         ++s.uses;
+        if (span_open) {
+            if (!s.span_t0) MVG_HIP(hipEventCreate(&s.span_t0));
+            if (!s.span_t1) MVG_HIP(hipEventCreate(&s.span_t1));
+            MVG_HIP(hipEventRecord(s.span_t0, s.stream));
+        }
         hipEvent_t t0 = nullptr, t1 = nullptr;
         if (timed) {
             if (s.ev_used == s.ev_pool.size()) {
@@ -1001,13 +1021,33 @@ int mvg_engine_multiply(mvg_engine* e) {
 int mvg_engine_sync(mvg_engine* e) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
     DeviceGuard g;
+    const bool span = e->timing_every == -1 && e->span_multiplies > 0;
     for (auto& s : e->shards) {
         MVG_HIP(hipSetDevice(s.device));
+        if (span && s.span_t1) MVG_HIP(hipEventRecord(s.span_t1, s.stream));
         MVG_HIP(hipStreamSynchronize(s.copy_stream));
         MVG_HIP(hipStreamSynchronize(s.stream));
         if (s.xstream) MVG_HIP(hipStreamSynchronize(s.xstream));
     }
     e->x_pending = false;
+    if (span) {
+        // the span's GEMV time per multiply: first GEMV's start to the stream's end, max over
+        // the local devices (the GEMV stream holds nothing else at one rank per process; with an
+        // exchange it also holds the once-per-ring waits on the exchange stream)
+        float worst = 0.f;
+        for (auto& s : e->shards) {
+            if (!s.span_t0 || !s.span_t1) continue;
+            float ms = 0.f;
+            MVG_HIP(hipEventElapsedTime(&ms, s.span_t0, s.span_t1));
+            worst = std::max(worst, ms);
+        }
+        if (e->span_valid) {
+            e->kernel_ms_sum += worst;
+            e->kernel_launches += e->span_multiplies;
+        }
+        e->span_multiplies = 0;
+        e->span_valid = true;
+    }
     if (e->timing_every > 0) {
         // per timed multiply call: max over local devices, then summed
         size_t n = e->shards.empty() ? 0 : e->shards[0].ev_used;

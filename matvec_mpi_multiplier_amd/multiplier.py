@@ -359,7 +359,8 @@ class Multiplier:
         return v.value
 
     def kernel_timing(self, every: int) -> None:
-        """Bracket every `every`-th multiply's GEMV with HIP events (0 = off)."""
+        """Bracket every `every`-th multiply's GEMV with HIP events (0 = off); -1 times spans of
+        back-to-back multiplies, one event pair from the first GEMV to the next sync."""
         check(lib.mvg_engine_kernel_timing(self.handle, int(every)), "mvg_engine_kernel_timing")
 
     def kernel_ms(self) -> KernelTiming:

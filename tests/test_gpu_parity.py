@@ -625,3 +625,28 @@ def test_library_and_pytorch_share_the_device_in_any_order():
         r = subprocess.run([sys.executable, "-c", code.format(repo=REPO_ROOT, first=first, second=second)],
                            capture_output=True, text=True, timeout=180)
         assert r.returncode == 0 and r.stdout.startswith("ok 1000.0"), r.stderr[-2000:]
+
+
+def test_span_kernel_timing_agrees_with_per_launch_events(comm1):
+    """mvg_engine_kernel_timing(-1): one event pair from the first GEMV of the span to the next
+    sync, averaged over its multiplies; it must agree with events on every launch (config 2's
+    shape, the bench's headline kernel) and reset at kernel_timing()."""
+    R = C = 16384
+    with mm.Multiplier("rowwise", R, C, comm1) as e:
+        e.fill_synth()
+        for _ in range(30):
+            e.multiply()
+        e.kernel_timing(1)
+        for _ in range(30):
+            e.multiply()
+        per_launch = e.kernel_ms()
+        e.kernel_timing(-1)
+        for _ in range(30):
+            e.multiply()
+        e.sync()
+        for _ in range(20):  # a second span after the sync adds up with the first
+            e.multiply()
+        span = e.kernel_ms()
+        e.kernel_timing(0)
+    assert per_launch.launches == 30 and span.launches == 50
+    assert 0.2 < span.avg_ms < 0.5 and abs(span.avg_ms - per_launch.avg_ms) <= 0.05 * per_launch.avg_ms, (span, per_launch)
