@@ -456,3 +456,25 @@ def test_an_uncaught_error_still_writes_the_line_so_far(tmp_path):
     d = json.loads(line)
     assert d["value"] == 42.0 and d["truncated"] is True and d["truncated_by"] == "error"
     assert d["truncated_in"] == "config 4 end_to_end" and d["error"].startswith("MemoryError")
+
+
+def test_a_budget_skip_still_gives_one_line_with_the_marker(tmp_path):
+    """A run whose budget runs out after the headline: the sections that no longer fit are
+    skipped, each marked in its place, and the process still prints exactly one JSON line."""
+    child = tmp_path / "rank0.py"
+    child.write_text(f"import sys\nsys.path.insert(0, {REPO!r})\nimport bench\n"
+                     "b = bench.Budget(b_used := bench.Budget(0).used() + 3.0)\n"
+                     "r = bench.Report(sys.stdout, b)\n"
+                     "r.update({'metric': bench.METRIC, 'value': 7184.6})\n"
+                     "r['exact'] = b.run('exact', 0.5, lambda: {'value': 7000.0})\n"
+                     "r['end_to_end'] = b.run('end_to_end', 600.0, lambda: {'mean_s': 0.04})\n"
+                     "r['configs'] = [dict(config='config 4', **b.run('config 4', 900.0, lambda: {}))]\n"
+                     "r.write()\n")
+    p = subprocess.run([sys.executable, str(child)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    (line,) = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    d = json.loads(line)
+    assert d["value"] == 7184.6 and d["exact"] == {"value": 7000.0} and "truncated" not in d
+    assert d["end_to_end"]["skipped"] == "budget" and d["end_to_end"]["need_s"] == 600.0
+    assert d["configs"][0]["skipped"] == "budget"
+    assert d["budget"]["skipped"] == ["end_to_end", "config 4"] and set(d["sections_s"]) == {"exact"}
