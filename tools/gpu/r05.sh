@@ -59,6 +59,12 @@ for step in $STEPS; do
       rc=$?; echo "mode $mode rc=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
     done
     cat $OUT/torch_probe.jsonl ;;
+  streamprobe)
+    echo "== tree kernel per stream, 4 processes"
+    for i in 1 2 3 4; do
+      timeout -k 10 120 python3 tools/probes/stream_probe.py 16384 16384 6 100 >> $OUT/stream_probe.jsonl 2>> $OUT/stream_probe.err || exit $?
+    done
+    cat $OUT/stream_probe.jsonl ;;
   rehearse8)
     echo "== N=8 same-device rehearsal with a 120 s budget (the launcher-free form: bench.py starts the ranks)"
     MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 120 \
