@@ -826,11 +826,11 @@ static bool even_refused() {
     return dev >= 0 && g_even_refused[dev].load(std::memory_order_relaxed) != 0;
 }
 
-// The errors with which the runtime turns down a launch's resources before dispatching it (the
-// LDS request above the CU's, a workgroup it cannot place); profiles/r05/p5a/lds_refusal.txt.
+// The errors with which the runtime turns down a launch's resources before dispatching it: the
+// LDS request above the CU's (hipErrorInvalidValue on ROCm 7, profiles/r05/p5a/lds_refusal.txt),
+// a workgroup shape or resource set it cannot place. Anything else is reported, never retried.
 static bool launch_refused(hipError_t e) {
-    return e == hipErrorInvalidValue || e == hipErrorInvalidConfiguration || e == hipErrorLaunchOutOfResources ||
-           e == hipErrorOutOfMemory;
+    return e == hipErrorInvalidValue || e == hipErrorInvalidConfiguration || e == hipErrorLaunchOutOfResources;
 }
 
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
