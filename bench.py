@@ -670,9 +670,15 @@ def est_exact(per_gpu, steps):
     return 4.0 + 3 * per_gpu / 6e12 * (2 * steps + 100)
 
 
+SHM_SETUP_GBPS = 0.8  # N > 1: the /dev/shm matrix (4 KiB tmpfs pages) filled by the ranks and page-locked
+                      # (r05 same-device rehearsal at N = 4: 137 GB in 153 s, 34 GB in 26 s)
+
+
 def est_e2e(total_bytes, n, iters, distributed):
-    gen = total_bytes / (GEN_GBPS * 1e9)
-    pin = total_bytes / (PIN_GBPS * 1e9)
+    if distributed:
+        gen, pin = total_bytes / (SHM_SETUP_GBPS * 1e9), 0.0
+    else:
+        gen, pin = total_bytes / (GEN_GBPS * 1e9), total_bytes / (PIN_GBPS * 1e9)
     per_iter = total_bytes / n / (H2D_GBPS * 1e9) + 0.05
     root_send = iters * total_bytes / (H2D_GBPS * 1e9) if distributed else 0.0
     return 4.0 + gen + pin + iters * per_iter + root_send

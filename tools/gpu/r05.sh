@@ -75,6 +75,11 @@ for step in $STEPS; do
     MVG_SAME_DEVICE=1 timeout -k 30 600 python3 bench.py --gpus 4 --steps 20 --warmup 5 \
         > $OUT/bench_n4.json 2> $OUT/bench_n4.err; rc=$?
     tail -c 600 $OUT/bench_n4.json; grep "bench:" $OUT/bench_n4.err | tail -8; ok $rc || exit $rc ;;
+  rehearse8d)
+    echo "== N=8 same-device rehearsal with the driver's defaults (budget 420 s; loopback sockets: the worst case)"
+    MVG_SAME_DEVICE=1 timeout -k 30 700 python3 bench.py --gpus 8 --steps 20 --warmup 5 \
+        > $OUT/bench_n8d.json 2> $OUT/bench_n8d.err; rc=$?
+    tail -c 600 $OUT/bench_n8d.json; grep "bench:" $OUT/bench_n8d.err | tail -8; ok $rc || exit $rc ;;
   sigterm8)
     echo "== N=8 same-device run terminated by a time limit mid-run: the line so far must come out (last step)"
     MVG_SAME_DEVICE=1 timeout -s TERM -k 60 75 python3 bench.py --gpus 8 --steps 5 --warmup 2 \
