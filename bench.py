@@ -16,8 +16,10 @@ every 5th step's GEMV bracketed; peak 8 TB/s; `traffic` from the committed rocpr
 summary when one matches this configuration), `cpu_baseline` (rank 0 at N = 1: the real
 reference, oracle/_ref under mpiexec, on a sample of the same matrix, with the oracle's
 restatement of its MPI loop on the full matrix beside it; the restatement alone when the
-reference cannot run), `end_to_end` (distribution from the root's host memory + multiply + y on
-the root, the reference's timing semantics), and `configs`: BASELINE.json configs 3-5 at their
+reference cannot run; its value from a sample beyond the host's L3), `end_to_end` (distribution
+from the root's host memory + multiply + y on the root, the reference's timing semantics; also
+under every config whose A fits the host memory measured at run time), and `configs`:
+BASELINE.json configs 3-5 at their
 own fixed sizes on the same N GPUs (strong scaling, device-resident, same engine, same step),
 so one scaling run covers every multi-GPU config (each also in bit-exact mode, `configs[].exact`);
 supplementary, never `value`. Each config carries `reference_rows` (its y against the real
@@ -34,7 +36,9 @@ Wall-time budget (--budget-s): the headline is timed first; every section after 
 that its estimated time fits in what is left of the budget (at N > 1 the decision is all-reduced,
 so every rank skips the same sections) and is recorded as {"skipped": "budget", ...} when it does
 not. `sections_s` holds each section's wall time. If rank 0 receives SIGTERM / SIGINT (a time
-limit around the run), it writes the line it has so far, marked "truncated": true, and exits.
+limit around the run) or an error ends the run, it writes the line it has so far, marked
+"truncated": true, and exits. `warnings` lists product paths that ran and failed without failing
+a check (the single-process executable at N > 1). Progress goes to stderr every 30 s.
 """
 from __future__ import annotations
 
