@@ -370,7 +370,7 @@ def test_bench_sigterm_mid_run_keeps_the_line(tmp_path):
     t.start()
     try:
         assert seen.wait(timeout=100), "".join(err[-20:])
-        time.sleep(3)  # inside config 4 (its fill, steps or the end-to-end host matrix)
+        time.sleep(1)  # inside config 4 (its fill, steps or the end-to-end host matrix)
         p.send_signal(signal.SIGTERM)
         out = p.stdout.read()
         assert p.wait(timeout=60) == 128 + signal.SIGTERM
