@@ -24,7 +24,7 @@ own fixed sizes on the same N GPUs (strong scaling, device-resident, same engine
 so one scaling run covers every multi-GPU config (each also in bit-exact mode, `configs[].exact`);
 supplementary, never `value`. Each config carries `reference_rows` (its y against the real
 reference's own y on four bands of its rows at P = N, tests/golden/config_slices.npz) and, at
-N = 1, a `cpu_baseline` of its own (the reference on a 64 MiB row slice, the -O2 port on the
+N = 1, a `cpu_baseline` of its own (the reference on a 512 MiB row slice, the -O2 port on the
 whole config up to 35 GB). `exact`: the same workload with the engine in bit-exact mode
 (mvg_engine_set_exact: y identical to the reference's sequential sums) — repeated multiplies on
 the engine's column-panel copy, and `row_major`, the kernels a fresh distribution runs — its step
@@ -98,8 +98,9 @@ def parse():
     ap.add_argument("--config-steps", type=int, default=20)
     ap.add_argument("--no-config-cpu-baseline", action="store_true",
                     help="skip the per-config CPU baselines (configs 3-5, N = 1)")
-    ap.add_argument("--config-ref-bytes", type=float, default=64 * 2 ** 20,
-                    help="size of the leading-row slice the real reference runs on per config (>= 128 rows)")
+    ap.add_argument("--config-ref-bytes", type=float, default=512 * 2 ** 20,
+                    help="size of the leading-row slice the real reference runs on per config (>= 128 rows; "
+                         "512 MiB: twice the L3 of the 16 CPUs its ranks use on the MI355X boxes)")
     ap.add_argument("--config-cpu-sample-bytes", type=float, default=3.5e10,
                     help="the port runs a config whole up to this size (configs 3, 5), else its leading rows")
     ap.add_argument("--config-cpu-seconds", type=float, default=4.0)
