@@ -701,13 +701,14 @@ def est_ref_run(nbytes, P):
     return 3.0 + nbytes / (REF_TEXT_GBPS * 1e9) / 10 + 100 * nbytes / rate
 
 
-def est_cpu_baseline(args, R, C, ref_rows=None, big_rows=None, sweep=True, port_bytes=None, cpu_seconds=None):
+def est_cpu_baseline(args, R, C, ref_rows=None, big_rows=None, sweep=True, port_bytes=None, cpu_seconds=None,
+                     placements=2):
     port_bytes = min(8 * R * C, args.cpu_sample_bytes if port_bytes is None else port_bytes)
     cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
     # inputs generated, the first timed iteration, then about cpu_seconds of iterations
     t = 3.0 + port_bytes / (6e9) + port_bytes / 4e9 + 2 * cpu_seconds
     small = 8 * min(R, ref_rows or args.ref_rows) * C
-    t += 2 * est_ref_run(small, 16)
+    t += placements * est_ref_run(small, 16)
     if sweep:
         t += sum(est_ref_run(small, p) for p in (1, 2, 4, 8))
     if big_rows:
@@ -1159,7 +1160,7 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
             entry["cpu_baseline"] = budget.run(
                 f"{name} cpu_baseline",
                 est_cpu_baseline(args, R, C, ref_rows=ref_rows, sweep=False, port_bytes=args.config_cpu_sample_bytes,
-                                 cpu_seconds=args.config_cpu_seconds),
+                                 cpu_seconds=args.config_cpu_seconds, placements=1),
                 guarded, cpu_baseline, args, alg, R, C, y, None, ref_rows, args.config_cpu_sample_bytes,
                 args.config_cpu_seconds, ("spread",), (), None, collective=False)
     return entry
