@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
     ap.add_argument("--cols", type=int, default=SHARD)
     ap.add_argument("--e2e-iters", type=int, default=3)
+    ap.add_argument("--settle-s", type=float, default=0.2,
+                    help="untimed multiplies (about this long) before the W warm-up steps: the GPU's clocks "
+                         "leave their idle state")
     ap.add_argument("--event-every", type=int, default=None,
                     help="kernel duration for the roofline: bracket every Nth step's GEMV with HIP events "
                          "(N > 0), or -1: one event pair spanning the timed steps' GEMVs (default -1 at one "
@@ -422,7 +425,8 @@ def main():
     if rank == 0:
         # from here on a time limit still gets a line: the fields known so far, "truncated": true
         report.update({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n, "steps": args.steps,
-                       "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                       "warmup": args.warmup, "settle_s": args.settle_s, "higher_is_better": True,
+                       "scaling": "weak", "vs_baseline": None,
                        "dtype": "f64",
                        "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text "
                                "inputs)"})
@@ -483,6 +487,14 @@ def main():
     eng.fill_synth()
     eng.sync()
 
+    # settle: a fresh process finds the GPU idle, and its clocks take a while to leave their idle
+    # state (round 4: the kernel's first launch after a 16 ms gap 322 us, then 300; round 5, one
+    # box: the headline's 20 steps at 311.5 us while the same shape ran 297 us later in the same
+    # process, profiles/r05/r5r). About --settle-s of untimed multiplies (the same count on every
+    # rank) run before the W warm-up steps, as every later section's warm-up does; recorded in
+    # the line as `settle_s`.
+    if args.settle_s > 0:
+        warm(eng, 1, distributed, local, seconds=args.settle_s)
     for _ in range(args.warmup):
         eng.multiply()
     eng.sync()

@@ -65,6 +65,16 @@ for step in $STEPS; do
       timeout -k 10 120 python3 tools/probes/stream_probe.py 16384 16384 6 100 >> $OUT/stream_probe.jsonl 2>> $OUT/stream_probe.err || exit $?
     done
     cat $OUT/stream_probe.jsonl ;;
+  settle)
+    echo "== headline only, fresh processes: settle 0 vs 0.2 s before the W = 5 warm-up steps, interleaved"
+    for i in 1 2 3 4 5 6; do for st in 0 0.2; do
+      timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --settle-s $st --no-exact --no-cpu-baseline --no-e2e \
+          --no-configs --no-multi --no-loader >> $OUT/settle.jsonl 2>> $OUT/settle.err || exit $?
+    done; done
+    python3 -c "
+import json
+for l in open('$OUT/settle.jsonl'):
+    d = json.loads(l); print(d['settle_s'], d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
   rehearse8)
     echo "== N=8 same-device rehearsal with a 120 s budget (the launcher-free form: bench.py starts the ranks)"
     MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 120 \
