@@ -75,6 +75,14 @@ for step in $STEPS; do
 import json
 for l in open('$OUT/settle.jsonl'):
     d = json.loads(l); print(d['settle_s'], d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
+  freshbox)
+    echo "== the first GPU process of the call: config 2's kernel over the first minute"
+    (rocm-smi --showmeminfo vram --showuse 2>&1 | tail -15) > $OUT/smi_before.txt
+    timeout -k 10 100 python3 tools/probes/fresh_box_probe.py 60 > $OUT/fresh_box.jsonl 2> $OUT/fresh_box.err || exit $?
+    python3 -c "
+import json
+rows = [json.loads(l) for l in open('$OUT/fresh_box.jsonl')]
+print([(r['t'], r['us']) for r in rows[:6]], '...', [(r['t'], r['us']) for r in rows[-3:]])" ;;
   rehearse8)
     echo "== N=8 same-device rehearsal with a 120 s budget (the launcher-free form: bench.py starts the ranks)"
     MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 120 \
