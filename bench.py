@@ -74,9 +74,11 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
     ap.add_argument("--cols", type=int, default=SHARD)
     ap.add_argument("--e2e-iters", type=int, default=3)
-    ap.add_argument("--settle-s", type=float, default=0.2,
-                    help="untimed multiplies (about this long) before the W warm-up steps: the GPU's clocks "
-                         "leave their idle state")
+    ap.add_argument("--settle-s", type=float, default=3.0,
+                    help="untimed multiplies before the W warm-up steps, at least this long (a fresh box's slow "
+                         "phase is itself steady, so time must outlast it) and until the per-step time is "
+                         "steady (0: none)")
+    ap.add_argument("--settle-max-s", type=float, default=10.0)
     ap.add_argument("--event-every", type=int, default=None,
                     help="kernel duration for the roofline: bracket every Nth step's GEMV with HIP events "
                          "(N > 0), or -1: one event pair spanning the timed steps' GEMVs (default -1 at one "
@@ -425,8 +427,7 @@ def main():
     if rank == 0:
         # from here on a time limit still gets a line: the fields known so far, "truncated": true
         report.update({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n, "steps": args.steps,
-                       "warmup": args.warmup, "settle_s": args.settle_s, "higher_is_better": True,
-                       "scaling": "weak", "vs_baseline": None,
+                       "warmup": args.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                        "dtype": "f64",
                        "data": "synthetic (splitmix64 k/10000 values, bit-identical to the reference's %.4f text "
                                "inputs)"})
@@ -487,14 +488,14 @@ def main():
     eng.fill_synth()
     eng.sync()
 
-    # settle: a fresh process finds the GPU idle, and its clocks take a while to leave their idle
-    # state (round 4: the kernel's first launch after a 16 ms gap 322 us, then 300; round 5, one
-    # box: the headline's 20 steps at 311.5 us while the same shape ran 297 us later in the same
-    # process, profiles/r05/r5r). About --settle-s of untimed multiplies (the same count on every
-    # rank) run before the W warm-up steps, as every later section's warm-up does; recorded in
-    # the line as `settle_s`.
-    if args.settle_s > 0:
-        warm(eng, 1, distributed, local, seconds=args.settle_s)
+    # settle: the first second or so of a fresh box runs the kernel slow (its clocks leaving
+    # idle; on a box just handed over, 310 us for ~1 s, then 296 — profiles/r05/fresh_box), and
+    # W = 5 warm-up steps (1.5 ms) do not cover it (round 5: the headline at 311.5 us while the
+    # same shape ran 297 us later in the same process, profiles/r05/r5r). So untimed multiplies
+    # run in bursts for at least --settle-s (3 s: the slow phase is steady in itself, so only time
+    # outlasts it) and until the per-step time is steady, at most --settle-max-s (settle()), then
+    # the W warm-up steps; the line records it as `settle`.
+    settled = settle(eng, args.settle_s, args.settle_max_s, distributed, local) if args.settle_s > 0 else None
     for _ in range(args.warmup):
         eng.multiply()
     eng.sync()
@@ -538,6 +539,7 @@ def main():
         expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, "y out of range")
         pmc = pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)) or {}
         report.update({
+            "settle": settled,
             "value": round(value, 1),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "gflops": round(2 * R * C * args.steps / elapsed / 1e9, 1),  # whole job, 2 flops per element of A
@@ -735,6 +737,35 @@ def est_loader(R, C):
 
 def est_single_process(R, C, n):
     return 30.0 + 60 * 8 * R * C / n / 7e12 + 8 * R * C / 20e9
+
+
+def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
+    """Untimed multiplies in bursts of `burst`, each timed by the wall clock between device syncs,
+    until the last three bursts' per-step times agree within `tol` and at least `min_s` has
+    passed, or `max_s` has (at N > 1 every rank runs bursts until every rank is done: the decision
+    is all-reduced, each multiply being a collective). Returns what it did: seconds, bursts, and
+    the first and last bursts' time per step."""
+    import torch
+    import torch.distributed as dist
+
+    t0, per = time.perf_counter(), []
+    while True:
+        tb = time.perf_counter()
+        for _ in range(burst):
+            e.multiply()
+        e.sync()
+        per.append((time.perf_counter() - tb) / burst)
+        el = time.perf_counter() - t0
+        last = per[-3:]
+        steady = len(last) == 3 and max(last) - min(last) <= tol * min(last)
+        done = el >= max_s or (el >= min_s and steady)
+        if distributed:
+            t = torch.tensor([1.0 if done else 0.0], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            done = float(t[0]) >= 1.0
+        if done:
+            return {"s": round(el, 2), "bursts": len(per), "steady": steady,
+                    "first_us_per_step": round(per[0] * 1e6, 1), "last_us_per_step": round(per[-1] * 1e6, 1)}
 
 
 def warm(e, min_launches, distributed, local, seconds=0.1):

@@ -478,3 +478,30 @@ def test_a_budget_skip_still_gives_one_line_with_the_marker(tmp_path):
     assert d["end_to_end"]["skipped"] == "budget" and d["end_to_end"]["need_s"] == 600.0
     assert d["configs"][0]["skipped"] == "budget"
     assert d["budget"]["skipped"] == ["end_to_end", "config 4"] and set(d["sections_s"]) == {"exact"}
+
+
+def test_settle_runs_until_the_step_time_is_steady():
+    """settle(): bursts of multiplies for at least min_s (a fresh box's slow first phase is
+    itself steady, so time must outlast it), then until three bursts agree, never longer than
+    max_s."""
+    import time
+
+    class Eng:
+        def __init__(self, slow_s):
+            self.t0 = time.perf_counter()
+            self.slow_s = slow_s
+            self.calls = 0
+
+        def multiply(self):
+            self.calls += 1
+            time.sleep(0.004 if time.perf_counter() - self.t0 < self.slow_s else 0.002)
+
+        def sync(self):
+            pass
+
+    e = Eng(0.3)
+    r = bench.settle(e, 0.35, 5.0, False, 0, burst=5, tol=0.25)
+    assert r["steady"] and 0.35 <= r["s"] < 2.0 and r["first_us_per_step"] > 1.5 * r["last_us_per_step"]
+    assert e.calls == 5 * r["bursts"]
+    r = bench.settle(Eng(10.0), 0.05, 0.2, False, 0, burst=5, tol=1e-9)  # never steady: stops at max_s
+    assert not r["steady"] and 0.2 <= r["s"] < 0.5

@@ -66,15 +66,15 @@ for step in $STEPS; do
     done
     cat $OUT/stream_probe.jsonl ;;
   settle)
-    echo "== headline only, fresh processes: settle 0 vs 0.2 s before the W = 5 warm-up steps, interleaved"
-    for i in 1 2 3 4 5 6; do for st in 0 0.2; do
+    echo "== headline only, fresh processes: no settle vs the settle before the W = 5 warm-up steps, interleaved"
+    for i in 1 2 3 4 5 6; do for st in ${SETTLE:-3} 0; do
       timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --settle-s $st --no-exact --no-cpu-baseline --no-e2e \
           --no-configs --no-multi --no-loader >> $OUT/settle.jsonl 2>> $OUT/settle.err || exit $?
     done; done
     python3 -c "
 import json
 for l in open('$OUT/settle.jsonl'):
-    d = json.loads(l); print(d['settle_s'], d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
+    d = json.loads(l); print(d.get('settle'), d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
   freshbox)
     echo "== the first GPU process of the call: config 2's kernel over the first minute"
     (rocm-smi --showmeminfo vram --showuse 2>&1 | tail -15) > $OUT/smi_before.txt
