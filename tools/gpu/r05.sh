@@ -74,7 +74,8 @@ for step in $STEPS; do
     python3 -c "
 import json
 for l in open('$OUT/settle.jsonl'):
-    d = json.loads(l); print(d.get('settle'), d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
+    d = json.loads(l); st = d.get('settle') or {}
+    print(st.get('s'), st.get('first_us_per_step'), d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
   freshbox)
     echo "== the first GPU process of the call: config 2's kernel over the first minute"
     (rocm-smi --showmeminfo vram --showuse 2>&1 | tail -15) > $OUT/smi_before.txt
