@@ -748,11 +748,11 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
     until the last three bursts' per-step times agree within `tol` and at least `min_s` has
     passed, or `max_s` has (at N > 1 every rank runs bursts until every rank is done: the decision
     is all-reduced, each multiply being a collective). Returns what it did: seconds, bursts, and
-    the first and last bursts' time per step."""
+    the first and last bursts' time per step, and a sample every 0.25 s."""
     import torch
     import torch.distributed as dist
 
-    t0, per = time.perf_counter(), []
+    t0, per, trace, next_mark = time.perf_counter(), [], [], 0.0
     while True:
         tb = time.perf_counter()
         for _ in range(burst):
@@ -760,6 +760,9 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
         e.sync()
         per.append((time.perf_counter() - tb) / burst)
         el = time.perf_counter() - t0
+        if el >= next_mark:  # a sample every 0.25 s: how long a slow phase lasted
+            trace.append([round(el, 2), round(per[-1] * 1e6, 1)])
+            next_mark += 0.25
         last = per[-3:]
         steady = len(last) == 3 and max(last) - min(last) <= tol * min(last)
         done = el >= max_s or (el >= min_s and steady)
@@ -769,7 +772,8 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
             done = float(t[0]) >= 1.0
         if done:
             return {"s": round(el, 2), "bursts": len(per), "steady": steady,
-                    "first_us_per_step": round(per[0] * 1e6, 1), "last_us_per_step": round(per[-1] * 1e6, 1)}
+                    "first_us_per_step": round(per[0] * 1e6, 1), "last_us_per_step": round(per[-1] * 1e6, 1),
+                    "trace_s_us": trace}
 
 
 def warm(e, min_launches, distributed, local, seconds=0.1):

@@ -75,7 +75,7 @@ for step in $STEPS; do
 import json
 for l in open('$OUT/settle.jsonl'):
     d = json.loads(l); st = d.get('settle') or {}
-    print(st.get('s'), st.get('first_us_per_step'), d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'])" ;;
+    print(st.get('s'), st.get('first_us_per_step'), d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'], st.get('trace_s_us', [])[:8])" ;;
   freshbox)
     echo "== the first GPU process of the call: config 2's kernel over the first minute"
     (rocm-smi --showmeminfo vram --showuse 2>&1 | tail -15) > $OUT/smi_before.txt
