@@ -749,9 +749,6 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
     passed, or `max_s` has (at N > 1 every rank runs bursts until every rank is done: the decision
     is all-reduced, each multiply being a collective). Returns what it did: seconds, bursts, and
     the first and last bursts' time per step, and a sample every 0.25 s."""
-    import torch
-    import torch.distributed as dist
-
     t0, per, trace, next_mark = time.perf_counter(), [], [], 0.0
     while True:
         tb = time.perf_counter()
@@ -767,6 +764,9 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
         steady = len(last) == 3 and max(last) - min(last) <= tol * min(last)
         done = el >= max_s or (el >= min_s and steady)
         if distributed:
+            import torch
+            import torch.distributed as dist
+
             t = torch.tensor([1.0 if done else 0.0], dtype=torch.float64, device=f"cuda:{local}")
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             done = float(t[0]) >= 1.0
