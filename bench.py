@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="global rows (default 16384*N)")
     ap.add_argument("--cols", type=int, default=SHARD)
     ap.add_argument("--e2e-iters", type=int, default=3)
-    ap.add_argument("--settle-s", type=float, default=3.0,
+    ap.add_argument("--settle-s", type=float, default=1.5,
                     help="untimed multiplies before the W warm-up steps, at least this long (a fresh box's slow "
                          "phase is itself steady, so time must outlast it) and until the per-step time is "
                          "steady (0: none)")
@@ -492,9 +492,10 @@ def main():
     # idle; on a box just handed over, 310 us for ~1 s, then 296 — profiles/r05/fresh_box), and
     # W = 5 warm-up steps (1.5 ms) do not cover it (round 5: the headline at 311.5 us while the
     # same shape ran 297 us later in the same process, profiles/r05/r5r). So untimed multiplies
-    # run in bursts for at least --settle-s (3 s: the slow phase is steady in itself, so only time
-    # outlasts it) and until the per-step time is steady, at most --settle-max-s (settle()), then
-    # the W warm-up steps; the line records it as `settle`.
+    # run in bursts for at least --settle-s (1.5 s: the slow phase is steady in itself, so only
+    # time outlasts it; under continuous load it lasted 0.5-0.75 s, profiles/r05/settle/) and until
+    # the per-step time is steady, at most --settle-max-s (settle()), then the W warm-up steps; the
+    # line records it as `settle`, with a sample of the step time every 0.25 s.
     settled = settle(eng, args.settle_s, args.settle_max_s, distributed, local) if args.settle_s > 0 else None
     # the W warm-up steps already run with kernel timing on, so the timing events' first use (their
     # creation, the runtime's first timestamped marker) falls outside the timed region
