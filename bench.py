@@ -498,14 +498,15 @@ def main():
     # line records it as `settle`, with a sample of the step time every 0.25 s.
     settled = settle(eng, args.settle_s, args.settle_max_s, distributed, local) if args.settle_s > 0 else None
     # the W warm-up steps already run with kernel timing on, so the timing events' first use (their
-    # creation, the runtime's first timestamped marker) falls outside the timed region
+    # creation, the runtime's first timestamped marker) falls outside the timed region; the
+    # collection comes before them, so the GPU does not idle for it between the warm-up and the
+    # timed steps (an idle gap lets the clocks drop: the first launch after a 16 ms gap ran 322 us
+    # against 300, round 4)
+    gc.collect()
     eng.kernel_timing(args.event_every)
     for _ in range(args.warmup):
         eng.multiply()
-    eng.sync()
-
-    eng.kernel_timing(args.event_every)  # resets the counts: only the K timed steps below
-    gc.collect()
+    eng.kernel_timing(args.event_every)  # waits for the warm-up, resets the counts: only the K timed steps
     gc.disable()  # no collector pause inside the timed region (K = 20 steps are 6 ms)
     try:
         barrier()

@@ -67,7 +67,7 @@ for step in $STEPS; do
     cat $OUT/stream_probe.jsonl ;;
   settle)
     echo "== headline only, fresh processes: no settle vs the settle before the W = 5 warm-up steps, interleaved"
-    for i in 1 2 3 4 5 6; do for st in ${SETTLE:-3} 0; do
+    for i in 1 2 3 4 5 6; do for st in ${SETTLE:-1.5} 0; do
       timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --settle-s $st --no-exact --no-cpu-baseline --no-e2e \
           --no-configs --no-multi --no-loader >> $OUT/settle.jsonl 2>> $OUT/settle.err || exit $?
     done; done
