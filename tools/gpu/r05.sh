@@ -84,6 +84,16 @@ for l in open('$OUT/settle.jsonl'):
 import json
 rows = [json.loads(l) for l in open('$OUT/fresh_box.jsonl')]
 print([(r['t'], r['us']) for r in rows[:6]], '...', [(r['t'], r['us']) for r in rows[-3:]])" ;;
+  evcost)
+    echo "== headline only: does timing the kernel with HIP events slow the steps? span events vs none, interleaved"
+    for i in 1 2 3 4 5 6; do for ev in -1 0; do
+      timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --event-every $ev --no-exact --no-cpu-baseline --no-e2e \
+          --no-configs --no-multi --no-loader >> $OUT/evcost.jsonl 2>> $OUT/evcost.err || exit $?
+    done; done
+    python3 -c "
+import json
+for l in open('$OUT/evcost.jsonl'):
+    d = json.loads(l); print(d['roofline']['kernel_ms'], d['value'], d['ms_per_step'], (d.get('settle') or {}).get('last_us_per_step'))" ;;
   rehearse8)
     echo "== N=8 same-device rehearsal with a 120 s budget (the launcher-free form: bench.py starts the ranks)"
     MVG_SAME_DEVICE=1 timeout -k 30 400 python3 bench.py --gpus 8 --steps 5 --warmup 2 --budget-s 120 \
