@@ -79,7 +79,8 @@ for l in open('$OUT/settle.jsonl'):
   freshbox)
     echo "== the first GPU process of the call: config 2's kernel over the first minute"
     (rocm-smi --showmeminfo vram --showuse 2>&1 | tail -15) > $OUT/smi_before.txt
-    timeout -k 10 100 python3 tools/probes/fresh_box_probe.py 60 > $OUT/fresh_box.jsonl 2> $OUT/fresh_box.err || exit $?
+    timeout -k 10 100 python3 tools/probes/fresh_box_probe.py ${FRESH_S:-60} 16384 16384 ${FRESH_PAUSE:-0.5} > $OUT/fresh_box.jsonl 2> $OUT/fresh_box.err || exit $?
+    ls /sys/bus/pci/devices/*/pp_dpm_sclk > $OUT/dpm_files.txt 2>&1 || true
     python3 -c "
 import json
 rows = [json.loads(l) for l in open('$OUT/fresh_box.jsonl')]
