@@ -488,7 +488,7 @@ def main():
     eng.fill_synth()
     eng.sync()
 
-    # settle: the first second or so of a fresh box runs the kernel slow (its clocks leaving
+    # settle: the first second or so of a fresh box runs the kernel slow (its shader clock leaving
     # idle; on a box just handed over, 310 us for ~1 s, then 296 — profiles/r05/fresh_box), and
     # W = 5 warm-up steps (1.5 ms) do not cover it (round 5: the headline at 311.5 us while the
     # same shape ran 297 us later in the same process, profiles/r05/r5r). So untimed multiplies
@@ -496,19 +496,21 @@ def main():
     # time outlasts it; under continuous load it lasted 0.5-0.75 s, profiles/r05/settle/) and until
     # the per-step time is steady, at most --settle-max-s (settle()), then the W warm-up steps; the
     # line records it as `settle`, with a sample of the step time every 0.25 s.
-    settled = settle(eng, args.settle_s, args.settle_max_s, distributed, local) if args.settle_s > 0 else None
-    # the W warm-up steps already run with kernel timing on, so the timing events' first use (their
-    # creation, the runtime's first timestamped marker) falls outside the timed region; the
-    # collection comes before them, so the GPU does not idle for it between the warm-up and the
-    # timed steps (an idle gap lets the clocks drop: the first launch after a 16 ms gap ran 322 us
-    # against 300, round 4)
+    # From the settle to the end of the timed steps the GPU never idles for more than a
+    # synchronize: an idle gap of >= 10 ms before 20 launches (a sleep, or the 36 ms of a
+    # gc.collect()) slows them by 0.6-1.2 % as the shader clock dips (profiles/r05/idle_gap/), so
+    # the collection runs before the settle and the collector stays off until the timed steps end.
     gc.collect()
-    eng.kernel_timing(args.event_every)
-    for _ in range(args.warmup):
-        eng.multiply()
-    eng.kernel_timing(args.event_every)  # waits for the warm-up, resets the counts: only the K timed steps
-    gc.disable()  # no collector pause inside the timed region (K = 20 steps are 6 ms)
+    gc.disable()
     try:
+        settled = (settle(eng, args.settle_s, args.settle_max_s, distributed, local)
+                   if args.settle_s > 0 else None)
+        # the W warm-up steps already run with kernel timing on, so the timing events' first use
+        # (their creation, the runtime's first timestamped marker) falls outside the timed region
+        eng.kernel_timing(args.event_every)
+        for _ in range(args.warmup):
+            eng.multiply()
+        eng.kernel_timing(args.event_every)  # waits for the warm-up, resets the counts: only the K timed steps
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -778,12 +780,14 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
                     "trace_s_us": trace}
 
 
-def warm(e, min_launches, distributed, local, seconds=0.1):
+def warm(e, min_launches, distributed, local, seconds=0.3):
     """Untimed multiplies before a supplementary timed section: at least `min_launches`, and about
     `seconds` of them, so that the section is timed in a steady state rather than right after the
-    host work between sections (y checks, D2H copies) has idled the GPU: the first launches after
-    such a gap run slow (round 4 traces: the tree kernel's first launch after a 16 ms gap 322 us,
-    then 300). Every rank runs the same count (each multiply has a collective at N > 1)."""
+    host work between sections (y checks, D2H copies) has idled the GPU: the launches after such a
+    gap run slow (round 4 traces: the tree kernel's first launch after a 16 ms gap 322 us, then
+    300; round 5: 20 launches after a 10-200 ms gap 0.6-1.2 % slower, and 0.3 s of load before
+    them undoes it, profiles/r05/idle_gap/). Every rank runs the same count (each multiply has a
+    collective at N > 1)."""
     import torch
     import torch.distributed as dist
 
@@ -1296,10 +1300,10 @@ def reference_rows_check(name, alg, R, C, n, y, yx):
            "source": "tests/golden/config_slices.npz: oracle/_ref, mpiexec -n P, on 4 bands of the config's rows"
                      + ("" if key.endswith(f"/P{n}") else f" (reference run at {key.split('/')[-1]}: row sums do not depend on P)")}
     if yx is not None:
-        gc = mm_grid_cols(n) if alg == "blockwise" else 1
+        grid_cols = mm_grid_cols(n) if alg == "blockwise" else 1
         out["exact_bit_identical"] = bool(np.array_equal(yx[rows], want))
         out["exact_max_rel"] = float(np.max(np.abs(yx[rows] - want) / np.abs(want)))
-        if gc > 2:
+        if grid_cols > 2:
             out["exact_note"] = "grid of > 2 columns: the reference adds in message-arrival order"
     return out
 

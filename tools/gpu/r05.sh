@@ -85,6 +85,27 @@ for l in open('$OUT/settle.jsonl'):
 import json
 rows = [json.loads(l) for l in open('$OUT/fresh_box.jsonl')]
 print([(r['t'], r['us']) for r in rows[:6]], '...', [(r['t'], r['us']) for r in rows[-3:]])" ;;
+  gcorder)
+    # bench_prev.py: `git show 4544303:bench.py > bench_prev.py` at the repo root for the run (not committed)
+    echo "== headline only, interleaved: the collection after the settle (bench_prev.py) against before it (bench.py)"
+    for i in 1 2 3 4 5 6; do for b in bench_prev.py bench.py; do
+      timeout -k 10 120 python3 $b --steps 20 --warmup 5 --no-exact --no-cpu-baseline --no-e2e \
+          --no-configs --no-multi --no-loader | sed "s/^{/{\"script\": \"$b\", /" >> $OUT/gcorder.jsonl 2>> $OUT/gcorder.err || exit $?
+    done; done
+    python3 -c "
+import json
+for l in open('$OUT/gcorder.jsonl'):
+    d = json.loads(l); print(d['script'], d['value'], d['roofline']['kernel_ms'], d['ms_per_step'])" ;;
+  idlegap)
+    echo "== does an idle gap (sleep, gc.collect) before 20 launches change their per-launch times?"
+    timeout -k 10 120 python3 tools/probes/idle_gap_probe.py ${GAP_ROUNDS:-4} > $OUT/idle_gap.jsonl 2> $OUT/idle_gap.err || exit $?
+    python3 -c "
+import json, collections
+by = collections.defaultdict(list)
+for l in open('$OUT/idle_gap.jsonl'):
+    r = json.loads(l); by[str(r['gap'])].append(r)
+for g, rs in by.items():
+    print(g, [r['idle_ms'] for r in rs][:2], 'mean', [r['mean_us'] for r in rs], 'first5', [r['first5_us'] for r in rs], 'last5', [r['last5_us'] for r in rs], [r['sclk_after'] for r in rs][:2])" ;;
   evcost)
     echo "== headline only: does timing the kernel with HIP events slow the steps? span events vs none, interleaved"
     for i in 1 2 3 4 5 6; do for ev in -1 0; do
