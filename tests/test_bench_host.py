@@ -221,25 +221,30 @@ def test_pmc_summary_finds_the_committed_counters():
     assert bench.pmc_summary(3, 5, "rowblk_w4_r2_u8") is None
 
 
-def test_warm_runs_about_the_requested_time():
-    """warm(): at least `min_launches`, then enough more for ~`seconds` of multiplies."""
-    import time
+def test_warm_runs_about_the_requested_time(monkeypatch):
+    """warm(): at least `min_launches`, then enough more for ~`seconds` of multiplies (a fake
+    clock that advances 1 ms per multiply, so the count does not depend on the host's load)."""
+    clock = [0.0]
+    monkeypatch.setattr(bench.time, "perf_counter", lambda: clock[0])
 
     class Eng:
         calls = 0
 
         def multiply(self):
             Eng.calls += 1
-            time.sleep(0.001)
+            clock[0] += 0.001
 
         def sync(self):
             pass
 
     bench.warm(Eng(), 3, False, 0, seconds=0.03)
-    assert 3 <= Eng.calls and 20 <= Eng.calls <= 40, Eng.calls
+    assert 29 <= Eng.calls <= 30, Eng.calls
     Eng.calls = 0
     bench.warm(Eng(), 5, False, 0, seconds=0.0)
     assert Eng.calls == 5
+    Eng.calls = 0
+    bench.warm(Eng(), 2, False, 0)  # the default: 0.3 s of load before a supplementary section
+    assert 299 <= Eng.calls <= 300, Eng.calls  # int() of 0.3 / 0.001 in floating point
 
 
 def test_ref_sweep_reports_speedup_and_efficiency(monkeypatch):
@@ -480,28 +485,35 @@ def test_a_budget_skip_still_gives_one_line_with_the_marker(tmp_path):
     assert d["budget"]["skipped"] == ["end_to_end", "config 4"] and set(d["sections_s"]) == {"exact"}
 
 
-def test_settle_runs_until_the_step_time_is_steady():
+def test_settle_runs_until_the_step_time_is_steady(monkeypatch):
     """settle(): bursts of multiplies for at least min_s (a fresh box's slow first phase is
     itself steady, so time must outlast it), then until three bursts agree, never longer than
-    max_s."""
-    import time
+    max_s (a fake clock: 4 ms per multiply during the slow phase, 2 ms after)."""
+    clock = [0.0]
+    monkeypatch.setattr(bench.time, "perf_counter", lambda: clock[0])
 
     class Eng:
         def __init__(self, slow_s):
-            self.t0 = time.perf_counter()
+            self.t0 = clock[0]
             self.slow_s = slow_s
             self.calls = 0
 
         def multiply(self):
             self.calls += 1
-            time.sleep(0.004 if time.perf_counter() - self.t0 < self.slow_s else 0.002)
+            clock[0] += 0.004 if clock[0] - self.t0 < self.slow_s else 0.002
 
         def sync(self):
             pass
 
     e = Eng(0.3)
-    r = bench.settle(e, 0.35, 5.0, False, 0, burst=5, tol=0.25)
-    assert r["steady"] and 0.35 <= r["s"] < 2.0 and r["first_us_per_step"] > 1.5 * r["last_us_per_step"]
-    assert e.calls == 5 * r["bursts"]
-    r = bench.settle(Eng(10.0), 0.05, 0.2, False, 0, burst=5, tol=1e-9)  # never steady: stops at max_s
-    assert not r["steady"] and 0.2 <= r["s"] < 0.5
+    r = bench.settle(e, 0.35, 5.0, False, 0, burst=5, tol=0.01)
+    assert r["steady"] and 0.35 <= r["s"] < 0.4 and r["first_us_per_step"] == 4000.0
+    assert r["last_us_per_step"] == 2000.0 and e.calls == 5 * r["bursts"]
+    assert r["trace_s_us"][0] == [0.02, 4000.0]
+    r = bench.settle(Eng(10.0), 0.05, 0.2, False, 0, burst=5, tol=0.01)  # slow throughout: steady at once
+    assert r["steady"] and 0.05 <= r["s"] < 0.08
+    flip = Eng(0.0)
+    flip.multiply = lambda: clock.__setitem__(0, clock[0] + (0.002 if flip.calls % 2 else 0.003)) or setattr(
+        flip, "calls", flip.calls + 1)
+    r = bench.settle(flip, 0.05, 0.2, False, 0, burst=1, tol=1e-9)  # never steady: stops at max_s
+    assert not r["steady"] and 0.2 <= r["s"] < 0.21
