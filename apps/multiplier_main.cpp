@@ -350,6 +350,9 @@ int main(int argc, char** argv) {
                sum_time / iters, iters);
         printf("device-resident: %.4f ms per multiply, %.1f GB/s aggregate; GEMV kernel %.3f ms (max over GPUs)\n",
                dev_s * 1e3, bytes / dev_s / 1e9, kms);
+        int rccl_v = 0, hip_v = 0;
+        if (mvg_runtime_versions(&rccl_v, &hip_v) == MVG_OK)  // which RCCL / HIP this process runs on
+            printf("runtime: RCCL %d (%s), HIP %d (%s)\n", rccl_v, mvg_runtime_path(1), hip_v, mvg_runtime_path(0));
         if (ranks)
             printf("launch: %d ranks, one GPU each; distribution %s\n", comm_sz,
                    synth_device ? "none (inputs generated on every GPU)"

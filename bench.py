@@ -99,7 +99,9 @@ def parse():
                     help="rank counts the real reference also runs at on the headline sample (cpu_baseline.sweep), "
                          "besides the host's CPU quota; '' skips the sweep")
     ap.add_argument("--no-configs", action="store_true", help="skip the BASELINE configs 3-5 section")
-    ap.add_argument("--configs", default="3,4,5", help="which BASELINE configs the section runs, in order")
+    ap.add_argument("--configs", default="auto",
+                    help="which BASELINE configs the section runs, in order; auto: those BASELINE.json defines at "
+                         "this N first (N = 8: 5, 4, 3), then the rest smallest first (config_order)")
     ap.add_argument("--config-steps", type=int, default=20)
     ap.add_argument("--no-config-cpu-baseline", action="store_true",
                     help="skip the per-config CPU baselines (configs 3-5, N = 1)")
@@ -131,6 +133,49 @@ def log(*a):
 
 FAILURES: list[str] = []  # the bench's parity checks that failed (JSON `failures`; exit code 1)
 WARNINGS: list[str] = []  # product paths that ran and failed without failing a check (JSON `warnings`)
+CHILDREN: set = set()  # live child processes (each the leader of its own session): ended with the run
+
+
+def stop_children(grace_s: float = 5.0) -> None:
+    """End every live child's process group (the single-process executable driving N GPUs, the
+    reference under mpiexec): SIGTERM, then SIGKILL after `grace_s`. Called when a signal ends
+    the run, so a supervisor that signals only this process leaves nothing running."""
+    live = list(CHILDREN)
+    for p in live:
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except (ProcessLookupError, PermissionError):
+            pass
+    t0 = time.perf_counter()
+    for p in live:
+        try:
+            p.wait(timeout=max(0.1, grace_s - (time.perf_counter() - t0)))
+        except Exception:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+
+
+def run_child(cmd, timeout, **kw):
+    """subprocess.run(capture_output, text) in a session of its own, registered in CHILDREN
+    while it runs; its whole process group is killed at the time limit."""
+    import subprocess
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True, **kw)
+    CHILDREN.add(p)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.communicate()
+        raise
+    finally:
+        CHILDREN.discard(p)
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
 class Budget:
@@ -295,6 +340,7 @@ class Report:
                 where = self.budget.current if self.budget is not None else None
                 log(f"bench: {name} during {where or 'the run'}: writing the line so far")
                 self.write(truncated=True, truncated_by=name, truncated_in=where)
+                stop_children()
                 exit_fn(128 + b[0])
                 return
 
@@ -626,20 +672,31 @@ def main():
                 ex["bit_identical_to_port"] = same_port
                 ex["bit_identical_to_reference_sample"] = same_ref
 
-    # end-to-end: root's host A -> shards -> multiply -> y on the root
-    if not args.no_e2e and args.e2e_iters > 0:
-        e2e = section("end_to_end", est_e2e(total_bytes, n, args.e2e_iters, distributed), end_to_end, args, eng, mm,
-                      R, C, rank, distributed, barrier, y, total_bytes, local, budget)
-        if rank == 0:
-            report["end_to_end"] = e2e
+    # BASELINE configs 3-5 at their own sizes on these N GPUs, and the end-to-end loops (the
+    # headline's and the configs'), in three passes (config_passes): every config's
+    # device-resident steps first, then the end-to-end loops smallest A first, then (N = 1) the
+    # configs' CPU baselines. The main engine's HBM is released first (config 4 is 128 GiB per
+    # GPU at N = 1); the headline's end-to-end loop runs on a fresh engine of its own.
+    eng.destroy()
+    if rank == 0 and not args.no_configs:
+        report["configs"] = []
 
-    # BASELINE configs 3-5 at their own sizes on these N GPUs (the main engine's HBM is released
-    # first: config 4 is 128 GiB per GPU at N = 1); each config checks the budget itself
-    if not args.no_configs:
-        eng.destroy()
-        if rank == 0:
-            report["configs"] = []
-        baseline_configs(args, mm, comm, n, rank, local, distributed, barrier, budget, report, guarded)
+    def headline_e2e():
+        def run():
+            e = mm.Multiplier(args.alg, R, C, comm)
+            try:
+                return end_to_end(args, e, mm, R, C, rank, distributed, barrier, y, total_bytes, local, budget)
+            finally:
+                e.destroy()
+
+        return section("end_to_end", est_e2e(total_bytes, n, args.e2e_iters, distributed), run)
+
+    config_passes(
+        args, n, rank, budget, report,
+        run_device=lambda k: config_device(args, mm, comm, n, rank, local, distributed, barrier, budget, guarded, k),
+        run_e2e=lambda k, yk: config_e2e(args, mm, comm, n, rank, local, distributed, barrier, budget, guarded, k, yk),
+        run_cpu=lambda k, yk: config_cpu(args, budget, guarded, k, yk),
+        headline_e2e=headline_e2e, headline_bytes=8 * R * C)
 
     # several x per pass over A, rank 0 at N = 1
     if rank == 0 and n == 1 and not args.no_multi:
@@ -654,13 +711,20 @@ def main():
     if rccl is not None:
         rccl["caller_NCCL_DEBUG"] = caller_debug
     if rank == 0:
+        from matvec_mpi_multiplier_amd._lib import runtime_info
+
+        # the RCCL and HIP runtime the rank sections ran on (PyTorch's bundled copies when the
+        # package imported torch first, _lib._torch_first); the single-process child reports its own
+        rt = runtime_info()
+        report["runtime"] = rt
+        if rccl is not None:
+            rccl["version"], rccl["path"] = rt.get("rccl_version"), rt.get("rccl_path")
         report["rccl"] = rccl
         if args.alg == "rowwise" and C == SHARD and R >= SHARD:
             # the weak-scaled matrix's first 16384 rows are config 2's matrix (global index i*C + j),
             # and a row's sum does not depend on P: config 2's reference rows check every N
             report["reference_rows"] = reference_rows_check("config 2", "rowwise", R, C, n, y, y_exact)
 
-    eng.destroy()
     comm.destroy()
     if distributed:
         dist.destroy_process_group()
@@ -697,8 +761,11 @@ def est_exact(per_gpu, steps):
     return 4.0 + 3 * per_gpu / 6e12 * (2 * steps + 100)
 
 
-SHM_SETUP_GBPS = 0.8  # N > 1: the /dev/shm matrix (4 KiB tmpfs pages) filled by the ranks and page-locked
-                      # (r05 same-device rehearsal at N = 4: 137 GB in 153 s, 34 GB in 26 s)
+SHM_SETUP_GBPS = 4.0  # N > 1: the /dev/shm matrix (4 KiB tmpfs pages: shmem huge pages are off on the
+                      # boxes) filled by the ranks, each with its share of the CPU quota, and page-locked
+                      # (round 6 probe, 32 GiB: 6.4 GB/s fill + 53 GB/s pin at 4 x 4 threads, against
+                      # 1.45 GB/s when each of 4 ranks ran the whole 16-CPU quota's threads —
+                      # profiles/r06/host_setup/)
 
 
 def est_e2e(total_bytes, n, iters, distributed):
@@ -853,7 +920,7 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
         cmd = [exe, str(R), str(C)]
         t0 = time.perf_counter()
         limit = 300.0 if budget is None else max(10.0, min(300.0, budget.left() - 5.0))
-        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=limit)
+        r = run_child(cmd, limit, cwd=work, env=env)
         wall = time.perf_counter() - t0
         out = {"ran": True, "command": f"MVG_NGPUS={n} MVG_SYNTH=device MVG_ITERS={iters} "
                                       f"bin/multiplier_{args.alg} {R} {C}", "rc": r.returncode,
@@ -870,6 +937,7 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
         m2 = re.search(r"end-to-end \(([^)]*)\): mean ([\d.]+) s", r.stdout)
         if m2:
             out["end_to_end_s"] = float(m2.group(2))
+        out["runtime"] = parse_runtime_line(r.stdout)
         y = np.loadtxt(ypath, dtype=np.float64, ndmin=1)
         expect(y.shape == (R,), f"single-process y has {y.shape} elements, want {R}")
         if args.alg == "rowwise" and C == SHARD and R >= SHARD and y.shape == (R,):
@@ -879,6 +947,22 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
         return {"ran": False, "error": f"{type(exc).__name__}: {str(exc)[:300]}"}
     finally:
         shutil.rmtree(work, ignore_errors=True)
+
+
+def parse_runtime_line(text):
+    """The executables' "runtime: RCCL <code> (<path>), HIP <version> (<path>)" line (the RCCL
+    and HIP runtime that process ran on), as runtime_info() reports them; None without one."""
+    import re
+
+    from matvec_mpi_multiplier_amd._lib import rccl_version_text
+
+    m = re.search(r"runtime: RCCL (\d+) \(([^)]*)\), HIP (\d+) \(([^)]*)\)", text or "")
+    if not m:
+        return None
+    origin = (lambda p: "pytorch" if "/torch/lib/" in p else "rocm" if "/rocm" in p else "unknown")
+    return {"rccl_version": rccl_version_text(int(m.group(1))), "rccl_version_code": int(m.group(1)),
+            "rccl_path": m.group(2), "rccl_origin": origin(m.group(2)),
+            "hip_runtime_version": int(m.group(3)), "hip_path": m.group(4), "hip_origin": origin(m.group(4))}
 
 
 def exact_section(args, eng, n, rank, local, distributed, barrier, per_gpu, total_bytes, y_tree):
@@ -1070,58 +1154,148 @@ def exact_kernel_name(eng) -> str:
     return lib.mvg_gemv_exact_variant_name(lib.mvg_gemv_exact_auto_variant(sh.n_cols, sh.n_rows, sh.n_cols)).decode()
 
 
-# BASELINE.json configs[2..4], each at its own fixed size (strong scaling over N)
+# BASELINE.json configs[2..4], each at its own fixed size (strong scaling over N); the GPU
+# counts BASELINE.json quotes each one at ("across 1/2/4/8", "2x4 GPU grid", "at 8 GPUs")
 BASELINE_CONFIGS = [
     ("config 3", "colwise", 65536, 65536),
     ("config 4", "blockwise", 131072, 131072),
     ("config 5", "rowwise", 4194304, 512),
 ]
+DEFINED_AT = {3: (1, 2, 4, 8), 4: (8,), 5: (8,)}
 
 
-def baseline_configs(args, mm, comm, n, rank, local, distributed, barrier, budget=None, report=None, guarded=None):
-    """Configs 3-5 of BASELINE.json on the same N GPUs: device-resident synthetic inputs, one step
-    = GEMV on every shard + the algorithm's RCCL exchange (col: ncclReduce of R doubles; block:
-    row-communicator ncclReduce + leaders' ncclGather on the utils.c:26-37 grid, 2 x 4 at N = 8;
-    row: ncclGather), --config-steps steps timed between barriers, max over ranks. A config
-    whose shard does not fit in free HBM on every rank is skipped on all of them (the decision
-    is all-reduced so no rank waits in a collective another skipped), as is one whose estimate
-    no longer fits in the budget. Each finished config goes straight into `report` (rank 0), so
-    a truncated line keeps it."""
+def config_order(spec: str, n: int) -> list[int]:
+    """The configs the section runs, in order. An explicit list ("3,4,5") is kept as given;
+    "auto" puts the configs BASELINE.json defines at this N first, highest number first (at
+    N = 8: 5, 4, 3 — config 5 is the one defined only at 8 GPUs), then the others by per-GPU
+    bytes, smallest first (N = 1: 3, 5, 4)."""
+    if spec.strip() != "auto":
+        return [int(k) for k in spec.split(",") if k.strip()]
+    by_num = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}
+    defined = sorted((k for k in by_num if n in DEFINED_AT[k]), reverse=True)
+    rest = sorted((k for k in by_num if k not in defined), key=lambda k: by_num[k][2] * by_num[k][3])
+    return defined + rest
+
+
+def config_passes(args, n, rank, budget, report, run_device, run_e2e, run_cpu, headline_e2e=None,
+                  headline_bytes=0):
+    """BASELINE configs 3-5 in three passes, so that no end-to-end loop can cost a config its
+    device-resident number (round 5: the /dev/shm setup of configs 3 and 4 at N = 8 left no
+    budget for config 5):
+      1. every config's device-resident tree and exact steps, in config_order (run_device(k) ->
+         (entry, y): the entry goes into the line at once, y stays here for the later passes);
+      2. the end-to-end loops, smallest A first: the headline's (headline_e2e(), into the line's
+         `end_to_end`) and each config's in --config-e2e that has a device-resident y
+         (run_e2e(k, y) -> its `end_to_end`);
+      3. at N = 1, each config's CPU baseline (run_cpu(k, y) -> its `cpu_baseline`).
+    The passes' order and every skip are the same on every rank (run_* decide collectively).
+    Returns {k: entry}."""
+    by_num = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}
+    entries, ys = {}, {}
+    for k in config_order(args.configs, n) if not args.no_configs else []:
+        entry, y = run_device(k)
+        entries[k] = entry
+        if isinstance(entry, dict) and "value" in entry:
+            ys[k] = y
+        if rank == 0:
+            report.append("configs", entry)
+    e2e_set = {int(k) for k in args.config_e2e.split(",") if k.strip()}
+    jobs = []  # (bytes of A, order, what)
+    if headline_e2e is not None:
+        jobs.append((headline_bytes, 0, None))
+    for k in ys:
+        name, alg, R, C = by_num[k]
+        if k in e2e_set:
+            jobs.append((8 * R * C, k, k))
+        with report.lock:
+            entries[k]["end_to_end"] = ({"pending": "the end-to-end pass, after every config's device-resident steps"}
+                                        if k in e2e_set else "not requested (--config-e2e)")
+    if not args.no_e2e and args.e2e_iters > 0:
+        for _, _, k in sorted(jobs, key=lambda j: (j[0], j[1])):
+            if k is None:
+                got = headline_e2e()
+                if rank == 0:
+                    report["end_to_end"] = got
+                continue
+            got = run_e2e(k, ys[k])
+            with report.lock:
+                entries[k]["end_to_end"] = got
+    if n == 1 and rank == 0 and not args.no_cpu_baseline and not args.no_config_cpu_baseline:
+        for k in ys:
+            got = run_cpu(k, ys[k])
+            with report.lock:
+                entries[k]["cpu_baseline"] = got
+    return entries
+
+
+def config_device(args, mm, comm, n, rank, local, distributed, barrier, budget, guarded, k):
+    """Pass 1 for config k on the N GPUs: its shard must fit in free HBM on every rank (decided
+    collectively, like the budget) and its estimate in the budget; then one_config. Returns
+    (entry, y on rank 0 or None)."""
     import torch
     import torch.distributed as dist
 
-    budget = budget or Budget(float("inf"), distributed, f"cuda:{local}")
-    guarded = guarded or (lambda fn, *a: fn(*a))
-    out = []
-    by_num = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}
-    e2e_set = {int(k) for k in args.config_e2e.split(",") if k.strip()}
-    for k in (int(k) for k in args.configs.split(",") if k.strip()):
-        name, alg, R, C = by_num[k]
-        sh = mm.plan_shard(alg, R, C, n, rank)
-        part = R if alg == "colwise" else sh.y_len
-        need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + (9 + n) * part + R) + (1 << 30)  # + exact-mode gather buffer
-        free = torch.cuda.mem_get_info(local)[0]
-        ok = torch.tensor([1.0 if free >= need else 0.0], dtype=torch.float64, device=f"cuda:{local}")
-        if distributed:
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if float(ok[0]) < 1.0:
-            entry = {"config": name, "alg": alg, "R": R, "C": C, "skipped": f"needs {need >> 30} GiB of HBM per GPU"}
-        else:
-            per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
-            entry = budget.run(name, est_config(per, args.config_steps), guarded, one_config, args, mm, comm, n, rank,
-                               local, distributed, barrier, budget, guarded, name, alg, R, C, k in e2e_set)
-            if not isinstance(entry, dict) or "value" not in entry:
-                entry = {"config": name, "alg": alg, "R": R, "C": C, **(entry if isinstance(entry, dict) else {})}
-        out.append(entry)
-        if report is not None and rank == 0:
-            report.append("configs", entry)
-    return out
+    name, alg, R, C = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}[k]
+    sh = mm.plan_shard(alg, R, C, n, rank)
+    part = R if alg == "colwise" else sh.y_len
+    need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + (9 + n) * part + R) + (1 << 30)  # + exact-mode gather buffer
+    free = torch.cuda.mem_get_info(local)[0]
+    ok = torch.tensor([1.0 if free >= need else 0.0], dtype=torch.float64, device=f"cuda:{local}")
+    if distributed:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if float(ok[0]) < 1.0:
+        return {"config": name, "alg": alg, "R": R, "C": C, "skipped": f"needs {need >> 30} GiB of HBM per GPU"}, None
+    per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
+    got = budget.run(name, est_config(per, args.config_steps), guarded, one_config, args, mm, comm, n, rank,
+                     local, distributed, barrier, name, alg, R, C)
+    if isinstance(got, tuple):
+        return got
+    return {"config": name, "alg": alg, "R": R, "C": C, **(got if isinstance(got, dict) else {})}, None
 
 
-def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, guarded, name, alg, R, C, with_e2e):
-    """One BASELINE config on the N GPUs (baseline_configs): tree-mode steps, then — within the
-    budget and where host memory holds its A — the end-to-end loop, then the bit-exact steps; on
-    rank 0 its y against the reference's own rows and, at N = 1, its CPU baseline."""
+def config_e2e(args, mm, comm, n, rank, local, distributed, barrier, budget, guarded, k, y):
+    """Pass 2 for config k: north_star's end-to-end time — the root's host A distributed over
+    every GPU's link, multiplied, y on the root (the reference's timing semantics) — on a fresh
+    engine, wherever host memory (and /dev/shm at N > 1) holds A, measured now; y must equal
+    the device-resident y of pass 1 bit for bit (same values, same kernels)."""
+    name, alg, R, C = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}[k]
+    total = sum(8 * (s.n_rows * s.n_cols + s.n_cols + (R if alg == "colwise" else s.y_len))
+                for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
+    fit, mem = e2e_memory_fit(R, C, distributed, local, cap=int(args.host_mem_cap_gib * 2 ** 30))
+    if not fit:
+        return {"skipped": "memory", **mem}
+
+    def run():
+        e = mm.Multiplier(alg, R, C, comm)
+        try:
+            return end_to_end(args, e, mm, R, C, rank, distributed, barrier, y, total, local, budget)
+        finally:
+            e.destroy()
+
+    got = budget.run(f"{name} end_to_end", est_e2e(total, n, args.e2e_iters, distributed), guarded, run)
+    if isinstance(got, dict):
+        got.setdefault("host_memory", {}).update(mem)
+    return got
+
+
+def config_cpu(args, budget, guarded, k, y):
+    """Pass 3 for config k (rank 0, N = 1): the reference on a leading-row slice at the host's
+    core count, and the -O2 port on the whole config where host memory allows (config 4: its
+    leading rows), each checked against the device-resident y."""
+    name, alg, R, C = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}[k]
+    ref_rows = min(R, max(128, int(args.config_ref_bytes // (8 * C))))
+    return budget.run(
+        f"{name} cpu_baseline",
+        est_cpu_baseline(args, R, C, ref_rows=ref_rows, sweep=False, port_bytes=args.config_cpu_sample_bytes,
+                         cpu_seconds=args.config_cpu_seconds, placements=1),
+        guarded, cpu_baseline, args, alg, R, C, y, None, ref_rows, args.config_cpu_sample_bytes,
+        args.config_cpu_seconds, ("spread",), (), None, collective=False)
+
+
+def one_config(args, mm, comm, n, rank, local, distributed, barrier, name, alg, R, C):
+    """One BASELINE config's device-resident steps on the N GPUs (pass 1 of config_passes):
+    tree-mode steps, then the bit-exact steps; on rank 0 its y against the reference's own rows.
+    Returns (entry, y)."""
     import torch
     import torch.distributed as dist
 
@@ -1150,7 +1324,6 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
                 for s in (mm.plan_shard(alg, R, C, n, r) for r in range(n)))
     per = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + part)
     exact = None
-    e2e = None
     e = mm.Multiplier(alg, R, C, comm)
     try:
         e.fill_synth()
@@ -1161,19 +1334,6 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
         yx = None
         if rank == 0:
             expect(np.all(np.isfinite(y)) and y.min() >= 0.0 and y.max() <= C * 0.9999 ** 2, f"{name}: y out of range")
-        if with_e2e and not args.no_e2e and args.e2e_iters > 0:
-            # north_star's end-to-end time at every config: the root's host A distributed over
-            # every GPU's link, multiplied, y on the root (same values as the device-resident
-            # fill, so the exact steps below still multiply the same A), wherever host memory
-            # (and /dev/shm at N > 1) holds A, measured now
-            fit, mem = e2e_memory_fit(R, C, distributed, local, cap=int(args.host_mem_cap_gib * 2 ** 30))
-            if not fit:
-                e2e = {"skipped": "memory", **mem}
-            else:
-                e2e = budget.run(f"{name} end_to_end", est_e2e(total, n, args.e2e_iters, distributed), guarded,
-                                 end_to_end, args, e, mm, R, C, rank, distributed, barrier, y, total, local, budget)
-                if isinstance(e2e, dict):
-                    e2e["host_memory"] = mem
         if not args.no_exact:
             # the same config in bit-exact mode: exact kernels + the exact exchange (gather of
             # every partial to rank 0, the reference's combine order there)
@@ -1206,21 +1366,10 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, budget, gua
         "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
         "pmc": pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)),
         "exact": exact,
-        "end_to_end": e2e if with_e2e else "not requested (--config-e2e)",
     }
     if rank == 0:
         entry["reference_rows"] = reference_rows_check(name, alg, R, C, n, y, yx)
-        if n == 1 and not args.no_cpu_baseline and not args.no_config_cpu_baseline:
-            # the reference on a leading-row slice at the host's core count, and the -O2 port on
-            # the whole config where host memory allows (config 4: its leading rows)
-            ref_rows = min(R, max(128, int(args.config_ref_bytes // (8 * C))))
-            entry["cpu_baseline"] = budget.run(
-                f"{name} cpu_baseline",
-                est_cpu_baseline(args, R, C, ref_rows=ref_rows, sweep=False, port_bytes=args.config_cpu_sample_bytes,
-                                 cpu_seconds=args.config_cpu_seconds, placements=1),
-                guarded, cpu_baseline, args, alg, R, C, y, None, ref_rows, args.config_cpu_sample_bytes,
-                args.config_cpu_seconds, ("spread",), (), None, collective=False)
-    return entry
+    return entry, (y if rank == 0 else None)
 
 
 def host_mem_free() -> int:
@@ -1435,13 +1584,21 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
     out = {"semantics": "reference: root holds A, x in host memory; distribute + multiply + y on root"}
     from matvec_mpi_multiplier_amd.hostshare import SharedHostMatrix, shm_free_bytes
 
+    from matvec_mpi_multiplier_amd.hostshare import fill_threads
+
     shared = None
+    setup = {}  # this rank's host-matrix setup: fill (first touch) and page-locking, timed apart
+    t_fill = time.perf_counter()
     if not distributed:
         A = mm.synth_host(R, C, 42)
+        setup.update(rows=R, threads=host_threads(), fill_s=round(time.perf_counter() - t_fill, 3))
     else:
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", str(n_ranks(distributed))))
         shared = SharedHostMatrix.create(R, C, 42, f"bench_{os.environ.get('MASTER_PORT', '0')}",
-                                         device=f"cuda:{local}")
+                                         device=f"cuda:{local}", threads=fill_threads(local_ranks))
         A = shared.array if shared is not None else None
+        if shared is not None:
+            setup.update(shared.timing)
         if shared is None:
             out["shared"] = f"skipped: /dev/shm has {shm_free_bytes() >> 30} GiB free, needs {(R * C * 8) >> 30} GiB"
     x = mm.synth_host(1, C, 4242)[0]
@@ -1458,9 +1615,12 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
             reg = host_rows_region(A, sh.row_off, sh.row_off + sh.n_rows)
         else:
             reg = (A.ctypes.data, A.nbytes)
+        t_pin = time.perf_counter()
         if _l.mvg_host_register(*reg) != 0:
             reg = None
+        setup.update(pin_bytes=reg[1] if reg else 0, pin_s=round(time.perf_counter() - t_pin, 3))
     pinned = reg is not None
+    out["host_memory"] = host_setup_record(setup, distributed, C)
     if have_shared:
         out["shared"] = timed(lambda: (eng.distribute_shared(A, x), eng.multiply(), eng.collect())[2])
         out["shared"]["distribution"] = ("per-GPU H2D from " + ("shared " if distributed else "")
@@ -1493,6 +1653,26 @@ def end_to_end(args, eng, mm, R, C, rank, distributed, barrier, y_ref, total_byt
             link["frac_of_copy"] = round(per_gpu / link["h2d_copy_GBps"], 4)
         out["roofline"] = link
     return out
+
+
+def host_setup_record(mine, distributed, C):
+    """Every rank's host-matrix setup (rows filled, fill threads, fill and page-lock seconds),
+    gathered to rank 0, with the aggregate rates: the fill's bytes over the slowest rank's fill,
+    the page-locked bytes over the slowest rank's hipHostRegister."""
+    allr = [mine]
+    if distributed:
+        import torch.distributed as dist
+
+        allr = [None] * dist.get_world_size()
+        dist.all_gather_object(allr, mine)
+    rec = {"by_rank": allr}
+    rows = sum(r.get("rows", 0) for r in allr if r)
+    fill = max((r.get("fill_s", 0.0) for r in allr if r), default=0.0)
+    pin = max((r.get("pin_s", 0.0) for r in allr if r), default=0.0)
+    pinned = sum(r.get("pin_bytes", 0) for r in allr if r)
+    return {**rec, "fill_s": fill, "pin_s": pin, "pin_bytes": pinned,
+            "rows": rows, "fill_GBps": round(8 * rows * C / fill / 1e9, 2) if fill > 0 else None,
+            "pin_GBps": round(pinned / pin / 1e9, 2) if pin > 0 else None}
 
 
 def host_rows_region(A, r0, r1, page=4096):
@@ -1586,7 +1766,7 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
     for label in placements:
         cset = sets[label] if sets[label] is not None else cpuset.pick_compact(P, gpu_numa_node())
         try:
-            runs.append((label, cset, ref_runner.run(alg, rows, C, P, timeout=args.ref_timeout, cpus=cset,
+            runs.append((label, cset, ref_runner.run(alg, rows, C, P, timeout=args.ref_timeout, cpus=cset, track=CHILDREN,
                                                      rows=np.arange(rows))))
         except Exception as exc:  # the baseline must never sink the bench
             port.setdefault("reference_errors", []).append(f"{label}: {str(exc)[:200]}")
@@ -1629,13 +1809,14 @@ def cpu_baseline(args, alg, R, C, y_gpu, y_exact=None, ref_rows=None, sample_byt
         else:
             bbytes = 8 * (brows * C + C + brows)
             try:
-                rb = ref_runner.run(alg, brows, C, P, timeout=args.ref_timeout, cpus=cpus, rows=np.arange(brows))
+                rb = ref_runner.run(alg, brows, C, P, timeout=args.ref_timeout, cpus=cpus, rows=np.arange(brows),
+                                    track=CHILDREN)
                 relb = float(np.max(np.abs(y_gpu[:brows] - rb["y"]) / np.abs(rb["y"])))
                 expect(relb <= 1e-12, f"GPU y differs from the reference's own y (beyond-cache sample): {relb}")
                 pts = [{"P": P, "s_per_iter": round(rb["seconds"], 6), "GBps": round(bbytes / rb["seconds"] / 1e9, 3)}]
                 if P > 1 and 1 in sweep_ps:
                     try:
-                        r1 = ref_runner.run(alg, brows, C, 1, timeout=args.ref_timeout,
+                        r1 = ref_runner.run(alg, brows, C, 1, timeout=args.ref_timeout, track=CHILDREN,
                                             cpus=cpuset.pick(1, gpu_numa_node()), rows=np.arange(brows))
                         pts.insert(0, {"P": 1, "s_per_iter": round(r1["seconds"], 6),
                                        "GBps": round(bbytes / r1["seconds"] / 1e9, 3)})
@@ -1721,7 +1902,7 @@ def ref_sweep(args, alg, rows, C, P, seconds_at_P, label_at_P, ps, nbytes):
         if p == P or p > P or p < 1 or not _splits(alg, rows, C, p):
             continue
         try:
-            rr = ref_runner.run(alg, rows, C, p, timeout=args.ref_timeout, cpus=cpuset.pick(p, gpu_numa_node()),
+            rr = ref_runner.run(alg, rows, C, p, timeout=args.ref_timeout, cpus=cpuset.pick(p, gpu_numa_node()), track=CHILDREN,
                                 rows=np.arange(rows))
             times[p], where[p] = rr["seconds"], "spread"
         except Exception as exc:  # a sweep point must never sink the bench

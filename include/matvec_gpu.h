@@ -61,6 +61,17 @@ const char* mvg_version(void);
 const char* mvg_strerror(int code);
 const char* mvg_last_error(void);
 
+/* The runtimes this library is bound to in the calling process (no counterpart in the
+ * reference, whose MPI is fixed at build time). The library needs libamdhip64.so.7 and
+ * librccl.so.1 by soname, so a process that loaded another copy first (PyTorch's ROCm wheel
+ * bundles its own HIP and RCCL) runs the library on that copy. mvg_runtime_versions: RCCL's
+ * ncclGetVersion code (e.g. 22705 = 2.27.5) and HIP's hipRuntimeGetVersion; either pointer may
+ * be NULL. mvg_runtime_path: the file the bound copy was loaded from (which: 0 = the HIP
+ * runtime, 1 = RCCL), "" when unknown. Neither call runs anything on a device (asking for the
+ * HIP version may start the HIP runtime; mvg_runtime_path and the RCCL version do not). */
+int mvg_runtime_versions(int* rccl_version, int* hip_runtime_version);
+const char* mvg_runtime_path(int which);
+
 /* ------------------------------------------------------------------ planner (host only, no GPU)
  * get_2_most_closest_multipliers (src/utils.c:26-37): rows = largest d <= floor(sqrt(p))
  * with p % d == 0, cols = p / d.  p <= 0 -> MVG_E_INVALID. */

@@ -95,6 +95,8 @@ SIGNATURES = {
     "mvg_version": (C.c_char_p, []),
     "mvg_strerror": (C.c_char_p, [C.c_int]),
     "mvg_last_error": (C.c_char_p, []),
+    "mvg_runtime_versions": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "mvg_runtime_path": (C.c_char_p, [C.c_int]),
     "mvg_grid_shape": (C.c_int, [_i64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mvg_plan_shard": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.POINTER(Shard)]),
     "mvg_plan_exchange": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.c_int, C.POINTER(XStep), C.c_int,
@@ -188,6 +190,11 @@ def _torch_first() -> None:
         import torch  # noqa: F401
     except ImportError:
         pass
+    except Exception as exc:  # a broken install (a missing .so: OSError, ...): the library's own runtime
+        import sys
+
+        print(f"matvec_mpi_multiplier_amd: importing torch failed ({type(exc).__name__}: {str(exc)[:200]}); "
+              "the library runs on its own HIP runtime (/opt/rocm)", file=sys.stderr)
 
 
 def _load() -> C.CDLL:
@@ -213,6 +220,52 @@ def check(rc: int, where: str) -> None:
         detail = lib.mvg_last_error().decode(errors="replace")
         cls = IndivisibleError if rc == MVG_E_INDIVISIBLE else MvgError
         raise cls(rc, where, detail)
+
+
+def mapped_runtimes(maps_lines) -> dict:
+    """The files of the HIP runtime and RCCL mapped into a process, from its /proc/<pid>/maps
+    lines: {"libamdhip64": [paths], "librccl": [paths]} (more than one path per library: two
+    copies are loaded)."""
+    out: dict = {"libamdhip64": set(), "librccl": set()}
+    for line in maps_lines:
+        parts = line.split(None, 5)
+        if len(parts) < 6:
+            continue
+        path = parts[5].strip()
+        base = os.path.basename(path)
+        for key in out:
+            if base.startswith(key + ".so"):
+                out[key].add(path)
+    return {k: sorted(v) for k, v in out.items()}
+
+
+def rccl_version_text(code: int) -> str:
+    """ncclGetVersion's code as X.Y.Z (NCCL_VERSION_CODE: X*10000 + Y*100 + Z since 2.9)."""
+    return f"{code // 10000}.{code // 100 % 100}.{code % 100}" if code >= 10000 else f"{code // 1000}.{code // 100 % 10}.{code % 100}"
+
+
+def runtime_info(hip_version: bool = True) -> dict:
+    """Which HIP runtime and RCCL this process's library calls go to (mvg_runtime_versions /
+    mvg_runtime_path: the copies the library resolved), every copy mapped into the process
+    (/proc/self/maps), and whether they are PyTorch's bundled ones or /opt/rocm's."""
+    r, h = C.c_int(0), C.c_int(0)
+    rc = lib.mvg_runtime_versions(C.byref(r), C.byref(h) if hip_version else None)
+    hip_path = lib.mvg_runtime_path(0).decode(errors="replace")
+    rccl_path = lib.mvg_runtime_path(1).decode(errors="replace")
+    try:
+        with open("/proc/self/maps") as f:
+            mapped = mapped_runtimes(f)
+    except OSError:
+        mapped = None
+
+    def origin(p):
+        return "pytorch" if "/torch/lib/" in p else "rocm" if "/rocm" in p else ("unknown" if p else None)
+
+    return {"rccl_version": rccl_version_text(r.value) if rc == MVG_OK and r.value else None,
+            "rccl_version_code": r.value if rc == MVG_OK else None,
+            "hip_runtime_version": h.value if rc == MVG_OK and hip_version else None,
+            "hip_path": hip_path, "rccl_path": rccl_path,
+            "hip_origin": origin(hip_path), "rccl_origin": origin(rccl_path), "mapped": mapped}
 
 
 def ptr(a) -> int:

@@ -20,6 +20,7 @@
 // One process may drive several devices (mvg_comm_init_all: the executables) or exactly one
 // (mvg_comm_init_rank: one process per GPU under torch.distributed.run). Every collective
 // is issued for all local devices inside ncclGroupStart/End, so both models share one path.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <stdlib.h>
 #include <string.h>
@@ -487,6 +488,23 @@ struct TraceXOps final : XOps {
 }  // namespace
 
 extern "C" {
+
+// ------------------------------------------------------------------ bound runtimes
+int mvg_runtime_versions(int* rccl_version, int* hip_runtime_version) {
+    if (rccl_version) MVG_NCCL(ncclGetVersion(rccl_version));
+    if (hip_runtime_version) MVG_HIP(hipRuntimeGetVersion(hip_runtime_version));
+    return MVG_OK;
+}
+
+// The object that defines one symbol of each runtime as this library resolved it: the copy the
+// process actually calls, whichever loaded first with the same soname.
+const char* mvg_runtime_path(int which) {
+    const void* sym = which == 0 ? (const void*)&hipGetDeviceCount
+                    : which == 1 ? (const void*)&ncclGetVersion : nullptr;
+    Dl_info info;
+    if (!sym || dladdr(sym, &info) == 0 || !info.dli_fname) return "";
+    return info.dli_fname;
+}
 
 // ------------------------------------------------------------------ communicators
 int mvg_comm_unique_id(unsigned char out[MVG_UNIQUE_ID_BYTES]) {

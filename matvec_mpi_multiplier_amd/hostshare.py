@@ -14,6 +14,7 @@ matrix on one socket feeding eight GPUs across the inter-socket link.
 from __future__ import annotations
 
 import os
+import time
 from multiprocessing import resource_tracker, shared_memory
 
 import numpy as np
@@ -51,6 +52,20 @@ def device_numa_cpus(device: int) -> set[int] | None:
         return None
 
 
+def fill_threads(local_ranks: int) -> int:
+    """Fill threads per rank when `local_ranks` ranks share this node's CPUs: the process's CPU
+    quota (cgroup cpu.max, affinity) split evenly, at least 1. Without the split every rank
+    starts the whole quota's worth of threads, and N ranks oversubscribe the quota N times."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(period) > 0:
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(64, n) // max(1, local_ranks))
+
+
 def shm_free_bytes() -> int:
     try:
         st = os.statvfs(SHM_DIR)
@@ -69,9 +84,14 @@ class SharedHostMatrix:
         self.shm = shm
         self.owner = owner
         self.array = np.ndarray(shape, dtype=np.float64, buffer=shm.buf)
+        self.timing: dict = {}  # this rank's share of the setup: rows, threads, fill seconds
 
     @classmethod
-    def create(cls, R: int, C: int, seed: int, tag: str, device: str = "cpu", margin: int = 1 << 30):
+    def create(cls, R: int, C: int, seed: int, tag: str, device: str = "cpu", margin: int = 1 << 30,
+               threads: int | None = None):
+        """`threads`: the fill threads of this rank (default: the library's host thread count,
+        $MVG_THREADS or the process's CPU quota). Ranks sharing one node's CPUs should split them
+        (fill_threads())."""
         import torch
         import torch.distributed as dist
 
@@ -100,18 +120,29 @@ class SharedHostMatrix:
         # first touch: rank r fills rows [r*R/n, (r+1)*R/n) from its GPU's NUMA node
         n, r = dist.get_world_size(), dist.get_rank()
         r0, r1 = R * r // n, R * (r + 1) // n
+        t0 = time.perf_counter()
         if r1 > r0 and C:
             cpus = device_numa_cpus(int(str(device).split(":")[1])) if str(device).startswith("cuda:") else None
             keep = os.sched_getaffinity(0)
+            had = os.environ.get("MVG_THREADS")
             if cpus:
                 os.sched_setaffinity(0, cpus)
+            if threads:
+                os.environ["MVG_THREADS"] = str(threads)
             try:
                 check(lib.mvg_synth_fill_host(me.array[r0:].ctypes.data, C, r1 - r0, C, r0, 0, C, seed),
                       "mvg_synth_fill_host")
             finally:
                 if cpus:
                     os.sched_setaffinity(0, keep)
+                if threads:
+                    if had is None:
+                        os.environ.pop("MVG_THREADS", None)
+                    else:
+                        os.environ["MVG_THREADS"] = had
+        me.timing = {"rows": r1 - r0, "threads": threads, "fill_s": round(time.perf_counter() - t0, 3)}
         dist.barrier()
+        me.timing["fill_wait_s"] = round(time.perf_counter() - t0, 3)  # until every rank's share is in
         return me
 
     def close(self) -> None:

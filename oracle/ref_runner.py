@@ -66,8 +66,32 @@ def write_synth_rows(path: str, rows: np.ndarray, C: int, seed: int) -> None:
                 f.write(txt.tobytes())
 
 
+def run_tracked(cmd, timeout, track=None, **kw) -> subprocess.CompletedProcess:
+    """subprocess.run in a session of its own (mpiexec and its ranks form one process group):
+    the group is killed when the time limit passes, and while it runs the Popen sits in `track`
+    (a set), so a caller that is being terminated can end the group too (bench.py's watcher)."""
+    import signal
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True, **kw)
+    if track is not None:
+        track.add(p)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.communicate()
+        raise
+    finally:
+        if track is not None:
+            track.discard(p)
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
+
+
 def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str | None = None,
-        cpus: list[int] | None = None, rows: np.ndarray | None = None) -> dict:
+        cpus: list[int] | None = None, rows: np.ndarray | None = None, track: set | None = None) -> dict:
     """mpiexec -n P multiplier_<alg> R C in a scratch directory. Returns {"seconds": mean time
     per iteration as the reference printed it, "y": rank 0's y, "wall_s": whole run incl. text
     loading}. With `cpus`, mpiexec and every rank it starts (MPICH's hydra does not bind by
@@ -77,7 +101,8 @@ def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str |
     (matr_utils.c:86-96, multiplier_colwise.c:107-122, multiplier_blockwise.c:367), so y is the
     reference's own y for those rows of the full problem at the same P (whenever the column
     split is the same: row split, column split, and block split on grids that divide both).
-    Raises RuntimeError on any failure."""
+    `track`: a set that holds the run's Popen while it runs (run_tracked). Raises RuntimeError
+    on any failure."""
     if not available(alg):
         raise RuntimeError(f"reference executable or {MPIEXEC} missing")
     own = workdir is None
@@ -99,8 +124,7 @@ def run(alg: str, R: int, C: int, P: int, timeout: float = 300.0, workdir: str |
         cmd = [MPIEXEC, "-n", str(P), os.path.join(REF_BIN, f"multiplier_{alg}"), str(R), str(C)]
         t0 = time.perf_counter()
         pin = (lambda: os.sched_setaffinity(0, cpus)) if cpus else None
-        r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True, timeout=timeout,
-                           preexec_fn=pin)
+        r = run_tracked(cmd, timeout, track, cwd=work, env=env, preexec_fn=pin)
         wall = time.perf_counter() - t0
         if r.returncode != 0 or not os.path.exists(csv) or not os.path.exists(ypath):
             raise RuntimeError(f"reference {alg} P={P} failed (rc {r.returncode}): {r.stdout[-400:]} {r.stderr[-400:]}")

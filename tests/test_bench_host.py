@@ -170,7 +170,8 @@ def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path,
                     "assert os.environ.get('NCCL_DEBUG') == 'WARN' and 'NCCL_DEBUG_FILE' not in os.environ\n"
                     "open(os.environ['MVG_Y_OUT'], 'w').write('1.5\\n' * 64)\n"
                     "print('end-to-end (multiply + y on root; inputs generated on the GPUs, nothing distributed): mean 0.000100 s over 50 iterations')\n"
-                    "print('device-resident: 0.0500 ms per multiply, 123.4 GB/s aggregate; GEMV kernel 0.040 ms (max over GPUs)')\n")
+                    "print('device-resident: 0.0500 ms per multiply, 123.4 GB/s aggregate; GEMV kernel 0.040 ms (max over GPUs)')\n"
+                    "print('runtime: RCCL 22707 (/opt/rocm/lib/librccl.so.1), HIP 70226015 (/opt/rocm/lib/libamdhip64.so.7)')\n")
     fake.chmod(0o755)
 
     class A:
@@ -180,6 +181,7 @@ def test_single_process_section_runs_the_executable_and_reads_its_line(tmp_path,
     r = bench.single_process_section(A(), 8, R, C, {"NCCL_DEBUG": "WARN", "NCCL_DEBUG_FILE": None}, exe=str(fake))
     assert r["ran"] and r["rc"] == 0, r
     assert r["ms_per_step"] == 0.05 and r["value"] == 123.4 and r["kernel_ms"] == 0.04 and r["end_to_end_s"] == 0.0001
+    assert r["runtime"]["rccl_version"] == "2.27.7" and r["runtime"]["rccl_origin"] == "rocm"
     assert "reference_rows" not in r  # the column split's config-2 rows are not the weak-scaled row split's
     # a failing executable is recorded, never raised and not counted as a failed check (the
     # scaling line's exit code stays 0); a wrong y from a run that finished is counted
@@ -254,7 +256,7 @@ def test_ref_sweep_reports_speedup_and_efficiency(monkeypatch):
 
     secs = {1: 0.050, 2: 0.030, 4: 0.020, 8: 0.025}
 
-    def fake_run(alg, R, C, p, timeout=None, cpus=None, rows=None):
+    def fake_run(alg, R, C, p, timeout=None, cpus=None, rows=None, track=None):
         if p == 8:
             raise RuntimeError("mpiexec failed")
         return {"seconds": secs[p], "y": None, "wall_s": 1.0}
@@ -517,3 +519,133 @@ def test_settle_runs_until_the_step_time_is_steady(monkeypatch):
         flip, "calls", flip.calls + 1)
     r = bench.settle(flip, 0.05, 0.2, False, 0, burst=1, tol=1e-9)  # never steady: stops at max_s
     assert not r["steady"] and 0.2 <= r["s"] < 0.21
+
+
+def test_config_order_puts_the_configs_defined_at_this_n_first():
+    assert bench.config_order("auto", 8) == [5, 4, 3]  # all three are defined at 8 GPUs; 5 only there
+    assert bench.config_order("auto", 1) == [3, 5, 4]  # config 3 (1/2/4/8) first, then smallest first
+    assert bench.config_order("auto", 2) == [3, 5, 4] and bench.config_order("auto", 4) == [3, 5, 4]
+    assert bench.config_order("4,3", 8) == [4, 3]  # an explicit list is kept as given
+
+
+def _pass_args(**kw):
+    import argparse
+
+    a = argparse.Namespace(configs="auto", no_configs=False, config_e2e="3,4,5", no_e2e=False, e2e_iters=3,
+                           no_cpu_baseline=False, no_config_cpu_baseline=False)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_config_passes_keep_every_device_resident_number_when_end_to_end_does_not_fit(capsys):
+    """Round 5's N = 8 run with the driver's defaults lost config 5 to the /dev/shm setup of
+    configs 3 and 4. Now every config's device-resident steps run before any end-to-end loop:
+    with end-to-end estimates beyond the budget, every config still has its value and only
+    end-to-end entries are skipped; the end-to-end loops that do run go smallest A first."""
+    import io
+
+    b = bench.Budget(limit_s=bench.Budget(0).used() + 15.0, verbose=False)
+    rep = bench.Report(io.StringIO(), b)
+    rep["configs"] = []
+    calls = []
+    by = {int(c[0].split()[-1]): c for c in bench.BASELINE_CONFIGS}
+
+    def dev(k):
+        calls.append(("device", k))
+        got = b.run(by[k][0], 1.0, lambda: ({"config": by[k][0], "value": 100.0 + k}, np.full(4, float(k))))
+        return got
+
+    def e2e(k, y):
+        calls.append(("e2e", k))
+        assert y[0] == float(k)
+        need = 8 * by[k][2] * by[k][3] / 0.8e9  # the round-5 /dev/shm rate: minutes
+        return b.run(f"{by[k][0]} end_to_end", need, lambda: {"mean_s": 1.0})
+
+    def head():
+        calls.append(("e2e", "headline"))
+        return b.run("end_to_end", 1.0, lambda: {"mean_s": 0.01})
+
+    out = bench.config_passes(_pass_args(), 8, 0, b, rep, dev, e2e, lambda k, y: calls.append(("cpu", k)),
+                              headline_e2e=head, headline_bytes=8 * 8 * 16384 * 16384)
+    assert calls[:3] == [("device", 5), ("device", 4), ("device", 3)]
+    # end-to-end smallest A first: headline (17.2 GB at N = 8) before config 5 (17.2 GB), 3 (34 GB), 4 (137 GB)
+    assert calls[3:] == [("e2e", "headline"), ("e2e", 5), ("e2e", 3), ("e2e", 4)]
+    line = rep.snapshot()
+    assert [c["config"] for c in line["configs"]] == ["config 5", "config 4", "config 3"]
+    assert all("value" in c for c in line["configs"])
+    assert all(c["end_to_end"]["skipped"] == "budget" for c in line["configs"])
+    assert line["end_to_end"] == {"mean_s": 0.01}
+    assert set(b.skipped) == {"config 3 end_to_end", "config 4 end_to_end", "config 5 end_to_end"}
+    assert set(out) == {3, 4, 5}
+
+
+def test_config_passes_at_one_gpu_runs_the_cpu_baselines_last():
+    import io
+
+    b = bench.Budget(1e6, verbose=False)
+    rep = bench.Report(io.StringIO(), b)
+    rep["configs"] = []
+    calls = []
+
+    def dev(k):
+        calls.append(("device", k))
+        if k == 4:  # a config that does not fit in HBM: no later pass for it
+            return {"config": "config 4", "skipped": "needs 140 GiB of HBM per GPU"}, None
+        return {"config": f"config {k}", "value": 1.0}, np.zeros(2)
+
+    bench.config_passes(_pass_args(config_e2e="3"), 1, 0, b, rep, dev,
+                        lambda k, y: calls.append(("e2e", k)) or {"mean_s": 2.0},
+                        lambda k, y: calls.append(("cpu", k)) or {"value": 4.2}, headline_e2e=None)
+    assert calls == [("device", 3), ("device", 5), ("device", 4), ("e2e", 3), ("cpu", 3), ("cpu", 5)]
+    cfg = {c["config"]: c for c in rep.snapshot()["configs"]}
+    assert cfg["config 3"]["end_to_end"] == {"mean_s": 2.0} and cfg["config 3"]["cpu_baseline"] == {"value": 4.2}
+    assert cfg["config 5"]["end_to_end"].startswith("not requested") and "end_to_end" not in cfg["config 4"]
+    # the other ranks (N > 1) run the same device and end-to-end passes, never the CPU baselines
+    calls.clear()
+    bench.config_passes(_pass_args(config_e2e="3"), 2, 1, b, rep, dev,
+                        lambda k, y: calls.append(("e2e", k)) or {}, lambda k, y: calls.append(("cpu", k)))
+    assert calls == [("device", 3), ("device", 5), ("device", 4), ("e2e", 3)]
+
+
+def test_parse_runtime_line_of_the_executables():
+    out = ("device-resident: 0.0500 ms per multiply, 123.4 GB/s aggregate; GEMV kernel 0.040 ms (max over GPUs)\n"
+           "runtime: RCCL 22707 (/opt/rocm/lib/librccl.so.1), HIP 70226015 (/opt/rocm/lib/libamdhip64.so.7)\n")
+    r = bench.parse_runtime_line(out)
+    assert r["rccl_version"] == "2.27.7" and r["rccl_origin"] == "rocm" and r["hip_runtime_version"] == 70226015
+    assert r["hip_path"] == "/opt/rocm/lib/libamdhip64.so.7"
+    assert bench.parse_runtime_line("no such line") is None
+
+
+def test_host_setup_record_rates_follow_the_slowest_rank():
+    rec = bench.host_setup_record({"rows": 100, "threads": 4, "fill_s": 0.5, "pin_bytes": 8e8, "pin_s": 0.2}, False, 1000)
+    assert rec["fill_GBps"] == round(8 * 100 * 1000 / 0.5 / 1e9, 2) and rec["pin_GBps"] == 4.0
+    assert rec["by_rank"][0]["threads"] == 4
+
+
+def test_fill_threads_split_the_quota_over_local_ranks():
+    from matvec_mpi_multiplier_amd.hostshare import fill_threads
+
+    one = fill_threads(1)
+    assert one >= 1 and fill_threads(8) == max(1, one // 8) and fill_threads(10 ** 6) == 1
+
+
+def test_stop_children_ends_a_running_child_group():
+    """A SIGTERM to the bench ends its children too (the watcher calls stop_children): a child
+    started by run_child, with a grandchild in its session, is gone within the grace period."""
+    import threading
+    import time
+
+    got = {}
+    t = threading.Thread(target=lambda: got.update(r=bench.run_child(["sh", "-c", "sleep 60 & wait"], 120)))
+    t0 = time.perf_counter()
+    t.start()
+    for _ in range(100):
+        if bench.CHILDREN:
+            break
+        time.sleep(0.05)
+    assert bench.CHILDREN
+    bench.stop_children(grace_s=5.0)
+    t.join(timeout=10)
+    assert not t.is_alive() and got["r"].returncode != 0 and time.perf_counter() - t0 < 10
+    assert not bench.CHILDREN

@@ -486,3 +486,30 @@ def test_exact_even_form_needs_whole_rounds_of_workgroups(cu_count, cus):
         wgs = -(-m // 64)
         assert (v == "hop8e_l8_w2_u16_n8") == (wgs >= cus and wgs % cus == 0), (m, cus, v)
 
+
+
+def test_runtime_info_names_the_bound_rccl_and_hip():
+    """mvg_runtime_versions / mvg_runtime_path: the RCCL and HIP runtime this process's library
+    calls go to (no device needed). Imported after PyTorch (the package's default), both are
+    PyTorch's bundled copies, which satisfy the library's sonames."""
+    info = _lib.runtime_info(hip_version=False)
+    assert info["rccl_version_code"] and info["rccl_version"].count(".") == 2
+    assert os.path.exists(info["rccl_path"]) and os.path.exists(info["hip_path"])
+    assert os.path.basename(info["rccl_path"]).startswith("librccl.so")
+    assert os.path.basename(info["hip_path"]).startswith("libamdhip64.so")
+    # the bound copy is a mapped one, and only one copy of each is mapped
+    real = lambda p: os.path.realpath(p)  # noqa: E731
+    assert real(info["rccl_path"]) in {real(p) for p in info["mapped"]["librccl"]}
+    assert len(info["mapped"]["libamdhip64"]) == 1 and len(info["mapped"]["librccl"]) == 1
+    assert _lib.lib.mvg_runtime_path(7) == b""
+
+
+def test_mapped_runtimes_and_version_text():
+    maps = ["7f00-7f10 r-xp 00000000 08:01 123 /opt/rocm-7.2.0/lib/librccl.so.1.0.70200\n",
+            "7f10-7f20 r--p 00000000 08:01 124 /usr/lib/python3/torch/lib/librccl.so\n",
+            "7f20-7f30 r-xp 00000000 08:01 125 /usr/lib/python3/torch/lib/libamdhip64.so\n",
+            "7f30-7f40 rw-p 00000000 00:00 0 \n", "7f40-7f50 r-xp 00000000 08:01 126 /usr/lib/librccl-net.so\n"]
+    m = _lib.mapped_runtimes(maps)
+    assert m["librccl"] == ["/opt/rocm-7.2.0/lib/librccl.so.1.0.70200", "/usr/lib/python3/torch/lib/librccl.so"]
+    assert m["libamdhip64"] == ["/usr/lib/python3/torch/lib/libamdhip64.so"]
+    assert _lib.rccl_version_text(22707) == "2.27.7" and _lib.rccl_version_text(22606) == "2.26.6"

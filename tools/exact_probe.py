@@ -3,7 +3,7 @@ shape, for rocprofv3 counter passes (development tool).
 
     python tools/exact_probe.py [M] [K] [launches] [exact variant name, "auto" or "panels"]
 
-"panels": the shard is rewritten once into the engine's column-panel layout
+"tree": the tree-summed kernel alone (no exact launches). "panels": the shard is rewritten once into the engine's column-panel layout
 (mvg_panel_relayout, P = mvg_exact_panel_width or 256) and the exact launches run
 mvg_gemv_exact_panels on it.
 """
@@ -21,7 +21,7 @@ def main():
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     name = sys.argv[4] if len(sys.argv) > 4 else "auto"
     v = 0
-    if name not in ("auto", "panels"):
+    if name not in ("auto", "panels", "tree"):
         names = [lib.mvg_gemv_exact_variant_name(i).decode() for i in range(lib.mvg_gemv_exact_variant_count())]
         v = names.index(name)
     dA, dx, dy = mm.DeviceBuffer(M * K), mm.DeviceBuffer(K), mm.DeviceBuffer(M)
@@ -34,7 +34,8 @@ def main():
         check(lib.mvg_panel_relayout(dA.ptr, K, M, K, dAp.ptr, M * P, P, None), "relayout")
         exact = lambda: lib.mvg_gemv_exact_panels(dAp.ptr, M * P, P, dx.ptr, dy.ptr, M, K, 0, None)  # noqa: E731
     for _ in range(n):
-        check(exact(), "exact")
+        if name != "tree":
+            check(exact(), "exact")
         check(lib.mvg_gemv(dA.ptr, K, dx.ptr, dy.ptr, M, K, None), "tree")
     check(lib.mvg_stream_sync(None), "sync")
     print(f"exact_probe {M}x{K}: {n} launches of {name} and of the tree kernel")
