@@ -376,18 +376,25 @@ def pmc_summary(M: int, K: int, variant: str):
     per launch (`traffic`), VALU busy, L2 hit rate, memory-side read latency and reads in flight,
     or None when no summary matches."""
     fam = kernel_family(variant)
+    out, sources = {}, []
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "pmc_*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(path))
         except Exception:
             continue
         if d.get("kernel_family") == fam and d.get("M") == M and d.get("K") == K:
-            out = {k: (round(d[k], 4) if isinstance(d[k], float) else d[k]) for k in (
+            # the newest summary first; a field it lacks (a counter pass it did not run) from the
+            # next newest that has it
+            got = {k: (float(f"{d[k]:.5g}") if isinstance(d[k], float) else d[k]) for k in (
                 "hbm_bytes_per_launch", "traffic_over_algorithmic", "valu_busy", "l2_hit", "ea_read_latency_cyc",
-                "ea_reads_in_flight", "dram_read_frac") if d.get(k) is not None}
-            out["source"] = os.path.relpath(path, REPO)
-            return out
-    return None
+                "ea_reads_in_flight", "dram_read_frac", "utcl1_miss_rate") if d.get(k) is not None and k not in out}
+            if got:
+                out.update(got)
+                sources.append(os.path.relpath(path, REPO))
+    if not out:
+        return None
+    out["source"] = sources[0] if len(sources) == 1 else sources
+    return out
 
 
 def launcher_cmd(argv: list[str], n: int, port: int) -> list[str]:
