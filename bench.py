@@ -1158,7 +1158,11 @@ def exact_kernel_name(eng) -> str:
     if P:
         v = lib.mvg_gemv_exact_panel_auto_variant(sh.n_rows, sh.n_cols)
         return f"{lib.mvg_gemv_exact_panel_variant_name(v).decode()} (column panels, P = {P})"
-    return lib.mvg_gemv_exact_variant_name(lib.mvg_gemv_exact_auto_variant(sh.n_cols, sh.n_rows, sh.n_cols)).decode()
+    name = lib.mvg_gemv_exact_variant_name(lib.mvg_gemv_exact_auto_variant(sh.n_cols, sh.n_rows, sh.n_cols)).decode()
+    dev = int(os.environ.get("LOCAL_RANK", "0")) if os.environ.get("MVG_SAME_DEVICE") != "1" else 0
+    if lib.mvg_gemv_exact_even_refused(dev) == 1:  # the runtime turned down the evenly placed form here
+        name += " (evenly placed form refused by the runtime: one-wave forms)"
+    return name
 
 
 # BASELINE.json configs[2..4], each at its own fixed size (strong scaling over N); the GPU

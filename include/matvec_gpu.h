@@ -246,6 +246,11 @@ const char* mvg_gemv_exact_variant_name(int variant);
  * to the one-wave form (same sums); it also forgets earlier refusals. */
 int mvg_debug_set_cu_count(int n);
 int mvg_debug_set_exact_even_lds(int64_t bytes);
+/* 1 when the runtime has refused the evenly placed exact form's LDS on `device` in this process
+ * (a request above the device's per-workgroup LDS, confirmed against
+ * hipDeviceAttributeMaxSharedMemoryPerBlock, logged once on stderr): the auto dispatch there
+ * then runs the one-wave forms. 0 otherwise; MVG_E_INVALID for a device index outside 0..63. */
+int mvg_gemv_exact_even_refused(int device);
 
 /* The same bit-exact product over A in column panels (the engine's device layout in exact mode,
  * DESIGN §4b): panel p holds columns [p*P, p*P + P) of all m rows, row i of it at
@@ -322,7 +327,10 @@ int mvg_engine_stream(const mvg_engine* e, int local_index, void** stream);
  * one event before the first GEMV after a reset or a sync and one at the next mvg_engine_sync,
  * nothing between the GEMVs of the span (a bracketing marker stalls the stream around its
  * kernel), so the average is the span over its multiplies (the GEMVs back to back, with their
- * dispatch gaps; at more than one rank it also holds the GEMV stream's waits on the exchange). */
+ * dispatch gaps; at more than one rank it also holds the GEMV stream's waits on the exchange).
+ * A span that also holds other writes to the shard — a distribution, a synthetic fill, exact
+ * mode's panel relayout after the span's first GEMV, a chunked distribution's copies — is
+ * dropped: it adds no launches and no time to the average. */
 int mvg_engine_kernel_timing(mvg_engine* e, int every);
 int mvg_engine_kernel_ms(mvg_engine* e, double* avg_ms, int64_t* launches);
 int mvg_engine_destroy(mvg_engine* e);

@@ -134,6 +134,7 @@ SIGNATURES = {
     "mvg_debug_trace_exchange": (C.c_int, [C.c_int, _i64, _i64, C.c_int, C.c_int, C.POINTER(XCall), C.c_int,
                                            C.POINTER(C.c_int)]),
     "mvg_debug_set_exact_even_lds": (C.c_int, [_i64]),
+    "mvg_gemv_exact_even_refused": (C.c_int, [C.c_int]),
     "mvg_gemv_exact_variant_name": (C.c_char_p, [C.c_int]),
     "mvg_gemv_exact_panels": (C.c_int, [_p, _i64, _i64, _p, _p, _i64, _i64, C.c_int, _p]),
     "mvg_panel_relayout": (C.c_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p]),

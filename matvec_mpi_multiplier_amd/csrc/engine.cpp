@@ -775,8 +775,15 @@ int mvg_engine_stream(const mvg_engine* e, int i, void** stream) {
     return MVG_OK;
 }
 
+// A write of the shard (distribution, synthetic fill) while a kernel-timing span is open would
+// land on the GEMV stream between the span's events: the span no longer times GEMVs alone.
+static void void_open_span(mvg_engine* e) {
+    if (e->timing_every == -1 && e->span_multiplies > 0) e->span_valid = false;
+}
+
 int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
+    void_open_span(e);
     DeviceGuard g;
     int rc;
     for (auto& s : e->shards) {
@@ -807,6 +814,7 @@ int mvg_engine_fill_synth(mvg_engine* e, uint64_t seed_a, uint64_t seed_x) {
 // overlapping the next chunk's H2D with the current chunk's send.
 int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
+    void_open_span(e);
     DeviceGuard g;
     const int64_t C = e->C;
     Shard* root = nullptr;
@@ -911,6 +919,7 @@ int mvg_engine_distribute(mvg_engine* e, const double* A, const double* x) {
 int mvg_engine_distribute_shared(mvg_engine* e, const double* A, const double* x) {
     if (!e) return fail(MVG_E_INVALID, "null engine");
     if (!x || (!A && e->R * e->C > 0)) return fail(MVG_E_INVALID, "every rank needs the shared A and x");
+    void_open_span(e);
     for (auto& s : e->shards) s.panels_fresh = false, s.uses = 0;
     DeviceGuard g;
     int rc = distribute_direct(e, A, x);
@@ -975,6 +984,8 @@ int mvg_engine_multiply(mvg_engine* e) {
                 int rc = mvg_panel_relayout(s.dA, p.n_cols, p.n_rows, p.n_cols, s.dAp, s.pstride, s.panelP, s.stream);
                 if (rc != MVG_OK) return rc;
                 s.panels_fresh = true;
+                // a relayout after the span's first event would be counted as GEMV time
+                if (e->timing_every == -1 && !span_open) e->span_valid = false;
             }
         }
         const bool panels = e->exact && s.dAp && s.panels_fresh;

@@ -1818,6 +1818,7 @@ const char* mvg_gemv_variant_name(int v) {
 
 int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m,
                      int64_t k, int variant, void* stream) {
+    if (int rc = take_pending_error("mvg_gemv"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv: negative size");
     if (variant < 0 || variant >= kNumVariants) return fail(MVG_E_INVALID, "mvg_gemv: bad variant");
     hipStream_t s = (hipStream_t)stream;
@@ -1864,6 +1865,7 @@ const char* mvg_gemv_multi_variant_name(int v) {
 
 int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_t ldx, double* Y,
                            int64_t ldy, int64_t m, int64_t k, int nv, int variant, void* stream) {
+    if (int rc = take_pending_error("mvg_gemv_multi"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0 || nv < 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: negative size");
     if (variant < 0 || variant >= kNumMultiVariants) return fail(MVG_E_INVALID, "mvg_gemv_multi: bad variant");
     if (m == 0 || nv == 0) return MVG_OK;
@@ -1924,6 +1926,7 @@ int mvg_gemv_multi(const double* A, int64_t lda, const double* X, int64_t ldx, d
 }
 
 int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {
+    if (int rc = take_pending_error("mvg_stream_read"); rc != MVG_OK) return rc;
     if (!src || !sink || n < 0 || (n & 1) || ((uintptr_t)src % 16))
         return fail(MVG_E_INVALID, "mvg_stream_read: need even n, 16-B aligned src, sink");
     hipLaunchKernelGGL(stream_read_kernel, dim3(256 * 4), dim3(kBlock), 0, (hipStream_t)stream, src,
@@ -1934,6 +1937,7 @@ int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {
 
 int mvg_synth_fill_device(double* dst, int64_t ld, int64_t m, int64_t k, int64_t row_off,
                           int64_t col_off, int64_t ncols, uint64_t seed, void* stream) {
+    if (int rc = take_pending_error("mvg_synth_fill_device"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0 || ld < k || row_off < 0 || col_off < 0 || col_off + k > ncols)
         return fail(MVG_E_INVALID, "mvg_synth_fill_device: bad shape");
     if (m == 0 || k == 0) return MVG_OK;

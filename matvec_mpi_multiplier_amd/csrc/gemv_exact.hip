@@ -35,6 +35,8 @@
 // DPP, still in column order.
 #include <atomic>
 
+#include <stdio.h>
+
 #include "common.h"
 #include "lds_dma.h"
 
@@ -833,6 +835,22 @@ static bool launch_refused(hipError_t e) {
     return e == hipErrorInvalidValue || e == hipErrorInvalidConfiguration || e == hipErrorLaunchOutOfResources;
 }
 
+// A refusal error counts as the LDS refusal only when the request is above what the device
+// grants one workgroup (hipDeviceAttributeMaxSharedMemoryPerBlock: 160 KiB on gfx950); any other
+// failure with the same code is this launch's error and is reported. Unknown limit: taken as the
+// refusal (the one-wave form then computes the same sums).
+static bool lds_refusal_confirmed(hipError_t e, size_t lds) {
+    if (!launch_refused(e)) return false;
+    const int dev = current_device();
+    int max_lds = 0;
+    if (dev < 0 || hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
+        max_lds <= 0) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return lds > (size_t)max_lds;
+}
+
 static int pick_seq_variant(int64_t lda, int64_t M, int64_t K, bool aligned, bool lines) {
     if (lines && operands_ok(kVec16Lda23, lda, aligned) && M >= 32768 && K > 2048 && K < 65536)
         return kSeqManyRows;
@@ -896,8 +914,7 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
     // An error the caller's last HIP call left pending is that call's: reported here as it is
     // (this call fails, nothing launched), before any HIP call of ours could replace it, and
     // never mistaken for a refusal of this call's launch below.
-    if (const hipError_t pending = hipGetLastError(); pending != hipSuccess)
-        return hip_fail(pending, "mvg_gemv_exact: HIP error pending from an earlier call");
+    if (int rc = take_pending_error("mvg_gemv_exact"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact: negative size");
     if (variant < 0 || variant >= kNumSeqVariants || (variant > 0 && !kSeqVariants[variant].fn))
         return fail(MVG_E_INVALID, "mvg_gemv_exact: bad variant");
@@ -943,13 +960,22 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         // A runtime that turns down the evenly placed form's LDS reservation (the first launch of
         // the call, nothing of it dispatched) gets the same sums from the one-wave form, and the
         // dispatch keeps to the one-wave forms on this device from then on.
-        if (e != hipSuccess && variant == 0 && v == kHopEven && r0 == 0 && launch_refused(e)) {
-            if (const int dev = current_device(); dev >= 0) g_even_refused[dev].store(1, std::memory_order_relaxed);
+        if (e != hipSuccess && variant == 0 && v == kHopEven && r0 == 0 && lds_refusal_confirmed(e, lds)) {
+            const int dev = current_device();
+            if (dev >= 0 && g_even_refused[dev].exchange(1, std::memory_order_relaxed) == 0)
+                fprintf(stderr, "matvec_gpu: device %d refused %zu B of LDS for the exact kernel's evenly placed form "
+                                "(%s); the exact dispatch keeps to the one-wave forms on it\n",
+                        dev, lds, hipGetErrorString(e));
             return mvg_gemv_exact_variant(A, lda, x, y, m, k, kHopRows, stream);
         }
         MVG_HIP(e);
     }
     return MVG_OK;
+}
+
+int mvg_gemv_exact_even_refused(int device) {
+    if (device < 0 || device >= 64) return fail(MVG_E_INVALID, "mvg_gemv_exact_even_refused: bad device");
+    return g_even_refused[device].load(std::memory_order_relaxed) != 0;
 }
 
 int mvg_debug_set_cu_count(int n) {
@@ -1003,6 +1029,7 @@ static int panel_log2(int64_t P) {
 
 int mvg_panel_relayout(const double* A, int64_t lda, int64_t m, int64_t k, double* Ap, int64_t pstride, int64_t P,
                        void* stream) {
+    if (int rc = take_pending_error("mvg_panel_relayout"); rc != MVG_OK) return rc;
     const int lp = P > 0 ? panel_log2(P) : -1;
     if (m < 0 || k < 0 || lp < 0 || lda < k) return fail(MVG_E_INVALID, "mvg_panel_relayout: bad shape or panel width");
     if (m == 0 || k == 0) return MVG_OK;
@@ -1022,6 +1049,7 @@ int mvg_panel_relayout(const double* A, int64_t lda, int64_t m, int64_t k, doubl
 
 int mvg_gemv_exact_panels(const double* Ap, int64_t pstride, int64_t P, const double* x, double* y, int64_t m,
                           int64_t k, int variant, void* stream) {
+    if (int rc = take_pending_error("mvg_gemv_exact_panels"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: negative size");
     if (variant < 0 || variant >= kNumPanelVariants) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: bad variant");
     if (m == 0) return MVG_OK;

@@ -30,6 +30,13 @@ int hip_fail(hipError_t e, const char* what) {
     return MVG_E_HIP;
 }
 
+int take_pending_error(const char* where) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return MVG_OK;
+    t_err = std::string(where) + ": HIP error pending from an earlier call: " + hipGetErrorString(e);
+    return MVG_E_HIP;
+}
+
 // ------------------------------------------------------------------ host threads
 int host_thread_count() {
     if (const char* e = getenv("MVG_THREADS")) {

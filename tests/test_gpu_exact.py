@@ -10,6 +10,7 @@ the golden y the real reference wrote (tests/golden), wherever the reference is 
 (block split with more than two grid columns adds in message-arrival order; there the check is
 against the oracle's rank order, and within the tolerance against the reference).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -448,9 +449,13 @@ def test_exact_dispatch_falls_back_when_the_runtime_refuses_the_lds_reservation(
     y = mm.multiply_std_rowwise(A, x, exact=True)
     assert np.array_equal(y, want), max_rel(y, want)
     assert name() == "hop8_l8_w2_u16"  # the refusal is remembered for this device
+    dev = ctypes.c_int(0)
+    assert _hip_runtime().hipGetDevice(ctypes.byref(dev)) == 0
+    assert lib.mvg_gemv_exact_even_refused(dev.value) == 1  # and visible to the caller (bench records it)
     assert np.array_equal(mm.multiply_std_rowwise(A, x, exact=True), want)
     _lib.check(lib.mvg_debug_set_exact_even_lds(0), "even lds")  # forgets the refusal
-    assert name() == "hop8e_l8_w2_u16_n8"
+    assert name() == "hop8e_l8_w2_u16_n8" and lib.mvg_gemv_exact_even_refused(dev.value) == 0
+    assert lib.mvg_gemv_exact_even_refused(64) == _lib.MVG_E_INVALID
 
 
 def test_exact_call_reports_an_error_pending_from_an_earlier_call(exact_hooks):
@@ -473,4 +478,38 @@ def test_exact_call_reports_an_error_pending_from_an_earlier_call(exact_hooks):
         assert np.array_equal(dy.download(m), oracle.multiply_std_rowwise(A, x))
     finally:
         for b in (dA, dx, dy):
+            b.free()
+
+
+def test_every_launch_entry_reports_an_error_pending_from_an_earlier_call():
+    """The tree, multi-vector, exact, panel and relayout entry points all take an error an
+    earlier HIP call left pending first and report it as that call's (nothing launched), so the
+    same stale error is attributed the same way whichever kernel the engine calls next."""
+    lib = _lib.lib
+    m, k, P = 6144, 1024, 256
+    A = oracle.synth(m, k, 42)
+    x = oracle.synth(1, k, 4242)[0]
+    dA, dx, dy = mm.DeviceBuffer(m * k).upload(A), mm.DeviceBuffer(k).upload(x), mm.DeviceBuffer(2 * m)
+    dAp, dX = mm.DeviceBuffer(m * k), mm.DeviceBuffer(2 * k)
+    dX.upload(np.concatenate([x, x]))
+    calls = {
+        "mvg_gemv": lambda: lib.mvg_gemv(dA.ptr, k, dx.ptr, dy.ptr, m, k, None),
+        "mvg_gemv_multi": lambda: lib.mvg_gemv_multi(dA.ptr, k, dX.ptr, k, dy.ptr, m, m, k, 2, None),
+        "mvg_gemv_exact": lambda: lib.mvg_gemv_exact(dA.ptr, k, dx.ptr, dy.ptr, m, k, None),
+        "mvg_panel_relayout": lambda: lib.mvg_panel_relayout(dA.ptr, k, m, k, dAp.ptr, m * P, P, None),
+        "mvg_gemv_exact_panels": lambda: lib.mvg_gemv_exact_panels(dAp.ptr, m * P, P, dx.ptr, dy.ptr, m, k, 0, None),
+    }
+    try:
+        hip = _hip_runtime()
+        for where, call in calls.items():
+            _lib.check(lib.mvg_stream_sync(None), "sync")
+            assert hip.hipSetDevice(1 << 20) != 0  # no such device: leaves an error pending
+            rc = call()
+            err = lib.mvg_last_error().decode()
+            assert rc == _lib.MVG_E_HIP and err.startswith(where + ": HIP error pending"), (where, rc, err)
+            _lib.check(call(), where)  # the next call runs normally
+        _lib.check(lib.mvg_stream_sync(None), "sync")
+        assert np.array_equal(dy.download(m), oracle.multiply_std_rowwise(A, x))  # the panels' exact y
+    finally:
+        for b in (dA, dx, dy, dAp, dX):
             b.free()

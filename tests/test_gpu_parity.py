@@ -650,3 +650,44 @@ def test_span_kernel_timing_agrees_with_per_launch_events(comm1):
         e.kernel_timing(0)
     assert per_launch.launches == 30 and span.launches == 50
     assert 0.2 < span.avg_ms < 0.5 and abs(span.avg_ms - per_launch.avg_ms) <= 0.05 * per_launch.avg_ms, (span, per_launch)
+
+
+def test_span_kernel_timing_drops_a_span_that_holds_other_writes(comm1):
+    """A span that also holds a write of the shard — a synthetic fill, a distribution, exact
+    mode's panel relayout after the span's first GEMV — no longer times GEMVs alone: it adds
+    neither launches nor time; the spans around it still count."""
+    R = C = 8192
+    A = oracle.synth(R, C, 42)
+    x = oracle.synth(1, C, 4242)[0]
+    with mm.Multiplier("rowwise", R, C, comm1) as e:
+        e.fill_synth()
+        e.kernel_timing(-1)
+        for _ in range(5):
+            e.multiply()
+        e.sync()  # a clean span: 5 launches
+        e.multiply()
+        e.fill_synth()  # inside the open span
+        e.multiply()
+        e.sync()
+        e.multiply()
+        e.distribute(A, x)  # inside the open span
+        e.multiply()
+        assert e.kernel_ms().launches == 5
+        e.set_exact(True)
+        e.distribute(A, x)
+        e.multiply()
+        e.sync()  # exact, first multiply of a distribution: row-major kernels, no relayout (counted)
+        n = e.kernel_ms().launches
+        e.multiply()  # a span opened on the second multiply: the relayout runs before its first event
+        e.multiply()
+        e.sync()
+        n2 = e.kernel_ms().launches
+        assert e.exact_panel_width() == 256  # this shape runs exact mode on the column-panel copy
+        e.distribute(A, x)  # panels stale again
+        e.multiply()  # opens the span (row-major exact kernels)
+        e.multiply()  # the relayout runs after the span's first event: the span is dropped
+        e.sync()
+        n3 = e.kernel_ms().launches
+        e.set_exact(False)
+        e.kernel_timing(0)
+    assert n == 6 and n2 == 8 and n3 == 8
