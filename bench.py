@@ -768,11 +768,13 @@ def est_exact(per_gpu, steps):
     return 4.0 + 3 * per_gpu / 6e12 * (2 * steps + 100)
 
 
-SHM_SETUP_GBPS = 4.0  # N > 1: the /dev/shm matrix (4 KiB tmpfs pages: shmem huge pages are off on the
-                      # boxes) filled by the ranks, each with its share of the CPU quota, and page-locked
-                      # (round 6 probe, 32 GiB: 6.4 GB/s fill + 53 GB/s pin at 4 x 4 threads, against
-                      # 1.45 GB/s when each of 4 ranks ran the whole 16-CPU quota's threads —
-                      # profiles/r06/host_setup/)
+SHM_SETUP_GBPS = 3.0  # N > 1: the /dev/shm matrix (4 KiB tmpfs pages: shmem huge pages are off on the
+                      # boxes, no hugetlb pool) filled by the ranks, each with its share of the CPU
+                      # quota, then page-locked. Round 6 probes, 32 GiB: 3.4-6.8 GB/s for the whole
+                      # node at 1, 4 or 8 processes (the tmpfs page allocation, not the CPUs: first
+                      # touch, MADV_POPULATE_WRITE or pinning first all land there), against 1.45
+                      # GB/s when each of 4 ranks ran the whole quota's threads (round 5's 0.8 GB/s)
+                      # and 57-63 GB/s for the N = 1 anonymous (THP) matrix (profiles/r06/host_setup*)
 
 
 def est_e2e(total_bytes, n, iters, distributed):

@@ -10,8 +10,9 @@ Modes: anon (each process its own numpy rows), shm (one segment, first touch by 
 shm_falloc (each process posix_fallocate's its own byte range of the segment first, so the
 pages exist before the fill writes them), shm_populate (madvise(MADV_POPULATE_WRITE) on its
 range first), shm_pinfirst (hipHostRegister on its untouched range first — the kernel allocates
-the pages while pinning — then the fill writes pinned pages). T = 0: the 16-CPU quota split
-over the P processes.
+the pages while pinning — then the fill writes pinned pages), shm_perrank (each process its own
+segment for its rows: an MPI-3 shared window's per-rank segments; one tmpfs file per process).
+T = 0: the 16-CPU quota split over the P processes.
 """
 import json
 import os
@@ -40,6 +41,15 @@ def worker(args):
     if mode == "anon":
         A = np.empty((r1 - r0, C))
         base, nb, keep = A.ctypes.data, A.nbytes, A
+    elif mode == "shm_perrank":
+        size = (r1 - r0) * C * 8
+        fd = os.open(f"/dev/shm/{name}_{p}", os.O_CREAT | os.O_RDWR, 0o600)
+        os.ftruncate(fd, size)
+        m = mmap.mmap(fd, size)
+        os.close(fd)
+        os.unlink(f"/dev/shm/{name}_{p}")  # the mapping keeps it until the process ends
+        A = np.ndarray((r1 - r0, C), buffer=m)
+        base, nb, keep = A.ctypes.data, A.nbytes, (m, A)
     else:
         fd = os.open(f"/dev/shm/{name}", os.O_RDWR)
         size = R * C * 8
@@ -92,7 +102,7 @@ def main():
         for P in Ps:
             for T in Ts:
                 name = f"mvg_probe_{os.getpid()}"
-                if mode != "anon":
+                if mode not in ("anon", "shm_perrank"):
                     fd = os.open(f"/dev/shm/{name}", os.O_CREAT | os.O_RDWR, 0o600)
                     os.ftruncate(fd, R * C * 8)
                     os.close(fd)
@@ -105,7 +115,7 @@ def main():
                 for pr in procs:
                     pr.join()
                 wall = time.perf_counter() - t
-                if mode != "anon":
+                if mode not in ("anon", "shm_perrank"):
                     os.unlink(f"/dev/shm/{name}")
                 nb = R * C * 8
                 fill = max(r["fill_s"] + r["alloc_s"] for r in res)
