@@ -20,8 +20,9 @@ int hip_fail(hipError_t e, const char* what);
 
 // An error that an earlier HIP call on this thread left pending belongs to that call. Every
 // public launch entry point (tree, multi-vector, exact, panels, relayout, fill, stream read)
-// takes it first and reports it as such — the call fails, nothing is launched — so the
-// hipGetLastError after its own launch only ever sees that launch's error.
+// takes it after its argument checks (pure host logic) and before its first HIP call, and
+// reports it as such — the call fails, nothing is launched — so the hipGetLastError after its
+// own launch only ever sees that launch's error.
 int take_pending_error(const char* where);
 
 #define MVG_HIP(call)                                                     \

@@ -1818,20 +1818,20 @@ const char* mvg_gemv_variant_name(int v) {
 
 int mvg_gemv_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m,
                      int64_t k, int variant, void* stream) {
-    if (int rc = take_pending_error("mvg_gemv"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv: negative size");
     if (variant < 0 || variant >= kNumVariants) return fail(MVG_E_INVALID, "mvg_gemv: bad variant");
     hipStream_t s = (hipStream_t)stream;
     if (m == 0) return MVG_OK;
     if (!y) return fail(MVG_E_INVALID, "mvg_gemv: null y");
+    if (k > 0 && (!A || !x)) return fail(MVG_E_INVALID, "mvg_gemv: null A or x");
+    if (k > 0 && lda < k) return fail(MVG_E_INVALID, "mvg_gemv: lda < k");
+    if (int rc = take_pending_error("mvg_gemv"); rc != MVG_OK) return rc;  // before our first HIP call
     if (k == 0) {
         hipLaunchKernelGGL(zero_kernel, dim3((unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096)),
                            dim3(256), 0, s, y, m);
         MVG_HIP(hipGetLastError());
         return MVG_OK;
     }
-    if (!A || !x) return fail(MVG_E_INVALID, "mvg_gemv: null A or x");
-    if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv: lda < k");
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
     const bool aligned8 = ((uintptr_t)A % 8 == 0) && ((uintptr_t)x % 8 == 0);
     const bool lines = (uintptr_t)A % 128 == 0 && lda % 16 == 0;  // every row starts on a 128-B line
@@ -1865,12 +1865,12 @@ const char* mvg_gemv_multi_variant_name(int v) {
 
 int mvg_gemv_multi_variant(const double* A, int64_t lda, const double* X, int64_t ldx, double* Y,
                            int64_t ldy, int64_t m, int64_t k, int nv, int variant, void* stream) {
-    if (int rc = take_pending_error("mvg_gemv_multi"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0 || nv < 0) return fail(MVG_E_INVALID, "mvg_gemv_multi: negative size");
     if (variant < 0 || variant >= kNumMultiVariants) return fail(MVG_E_INVALID, "mvg_gemv_multi: bad variant");
     if (m == 0 || nv == 0) return MVG_OK;
     if (!Y || ldy < m || (k > 0 && (!A || !X || lda < k || ldx < k)))
         return fail(MVG_E_INVALID, "mvg_gemv_multi: null pointer or leading dimension too small");
+    if (int rc = take_pending_error("mvg_gemv_multi"); rc != MVG_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)X % 16 == 0) && lda % 2 == 0 && ldx % 2 == 0;
     if (!vec || k == 0) {  // odd lda/ldx or a view off 16 B (or k = 0): one vector at a time,
@@ -1926,9 +1926,9 @@ int mvg_gemv_multi(const double* A, int64_t lda, const double* X, int64_t ldx, d
 }
 
 int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {
-    if (int rc = take_pending_error("mvg_stream_read"); rc != MVG_OK) return rc;
     if (!src || !sink || n < 0 || (n & 1) || ((uintptr_t)src % 16))
         return fail(MVG_E_INVALID, "mvg_stream_read: need even n, 16-B aligned src, sink");
+    if (int rc = take_pending_error("mvg_stream_read"); rc != MVG_OK) return rc;
     hipLaunchKernelGGL(stream_read_kernel, dim3(256 * 4), dim3(kBlock), 0, (hipStream_t)stream, src,
                        n / 2, sink);
     MVG_HIP(hipGetLastError());
@@ -1937,11 +1937,11 @@ int mvg_stream_read(const double* src, int64_t n, double* sink, void* stream) {
 
 int mvg_synth_fill_device(double* dst, int64_t ld, int64_t m, int64_t k, int64_t row_off,
                           int64_t col_off, int64_t ncols, uint64_t seed, void* stream) {
-    if (int rc = take_pending_error("mvg_synth_fill_device"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0 || ld < k || row_off < 0 || col_off < 0 || col_off + k > ncols)
         return fail(MVG_E_INVALID, "mvg_synth_fill_device: bad shape");
     if (m == 0 || k == 0) return MVG_OK;
     if (!dst) return fail(MVG_E_INVALID, "mvg_synth_fill_device: null dst");
+    if (int rc = take_pending_error("mvg_synth_fill_device"); rc != MVG_OK) return rc;
     const int64_t blocks = m < 65536 ? m : 65536;
     hipLaunchKernelGGL(synth_fill_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
                        (hipStream_t)stream, dst, ld, m, k, row_off, col_off, ncols,

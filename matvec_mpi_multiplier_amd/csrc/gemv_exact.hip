@@ -911,10 +911,6 @@ int mvg_gemv_exact_auto_variant(int64_t lda, int64_t m, int64_t k) {
 
 int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double* y, int64_t m, int64_t k,
                            int variant, void* stream) {
-    // An error the caller's last HIP call left pending is that call's: reported here as it is
-    // (this call fails, nothing launched), before any HIP call of ours could replace it, and
-    // never mistaken for a refusal of this call's launch below.
-    if (int rc = take_pending_error("mvg_gemv_exact"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact: negative size");
     if (variant < 0 || variant >= kNumSeqVariants || (variant > 0 && !kSeqVariants[variant].fn))
         return fail(MVG_E_INVALID, "mvg_gemv_exact: bad variant");
@@ -925,6 +921,10 @@ int mvg_gemv_exact_variant(const double* A, int64_t lda, const double* x, double
         if (!A || !x) return fail(MVG_E_INVALID, "mvg_gemv_exact: null A or x");
         if (lda < k) return fail(MVG_E_INVALID, "mvg_gemv_exact: lda < k");
     }
+    // An error the caller's last HIP call left pending is that call's: reported here as it is
+    // (this call fails, nothing launched), before any HIP call of ours (the dispatch's device
+    // queries included) could replace it, and never mistaken for a refusal of the launch below.
+    if (int rc = take_pending_error("mvg_gemv_exact"); rc != MVG_OK) return rc;
     const bool aligned = ((uintptr_t)A % 16 == 0) && ((uintptr_t)x % 16 == 0);
     const bool lines = (uintptr_t)A % 128 == 0 && lda % 16 == 0;  // every row starts on a 128-B line
     const int v = variant == 0 ? pick_seq_variant(lda, m, k, aligned, lines) : variant;
@@ -1029,12 +1029,12 @@ static int panel_log2(int64_t P) {
 
 int mvg_panel_relayout(const double* A, int64_t lda, int64_t m, int64_t k, double* Ap, int64_t pstride, int64_t P,
                        void* stream) {
-    if (int rc = take_pending_error("mvg_panel_relayout"); rc != MVG_OK) return rc;
     const int lp = P > 0 ? panel_log2(P) : -1;
     if (m < 0 || k < 0 || lp < 0 || lda < k) return fail(MVG_E_INVALID, "mvg_panel_relayout: bad shape or panel width");
     if (m == 0 || k == 0) return MVG_OK;
     if (!A || !Ap) return fail(MVG_E_INVALID, "mvg_panel_relayout: null pointer");
     if (pstride < m * P && (k + P - 1) / P > 1) return fail(MVG_E_INVALID, "mvg_panel_relayout: pstride < m * P");
+    if (int rc = take_pending_error("mvg_panel_relayout"); rc != MVG_OK) return rc;
     const int64_t blocks = m < (1ll << 20) ? m : (1ll << 20);
     const bool v16 = (uintptr_t)A % 16 == 0 && (uintptr_t)Ap % 16 == 0 && lda % 2 == 0 && P % 2 == 0 && pstride % 2 == 0;
     if (v16)
@@ -1049,7 +1049,6 @@ int mvg_panel_relayout(const double* A, int64_t lda, int64_t m, int64_t k, doubl
 
 int mvg_gemv_exact_panels(const double* Ap, int64_t pstride, int64_t P, const double* x, double* y, int64_t m,
                           int64_t k, int variant, void* stream) {
-    if (int rc = take_pending_error("mvg_gemv_exact_panels"); rc != MVG_OK) return rc;
     if (m < 0 || k < 0) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: negative size");
     if (variant < 0 || variant >= kNumPanelVariants) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: bad variant");
     if (m == 0) return MVG_OK;
@@ -1067,6 +1066,7 @@ int mvg_gemv_exact_panels(const double* Ap, int64_t pstride, int64_t P, const do
     const int rw = kPanelVariants[v].rows;
     const int64_t blocks = (m + rw - 1) / rw;
     if (blocks >= (1ll << 31)) return fail(MVG_E_INVALID, "mvg_gemv_exact_panels: too many rows for one launch");
+    if (int rc = take_pending_error("mvg_gemv_exact_panels"); rc != MVG_OK) return rc;
     hipLaunchKernelGGL(kPanelVariants[v].fn, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, Ap, pstride, lp,
                        x, y, m, k);
     MVG_HIP(hipGetLastError());
