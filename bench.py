@@ -624,6 +624,7 @@ def main():
                 "l2_hit": pmc.get("l2_hit"),
                 "kernel": kernel_name(sh) + ", per GPU",
                 "kernel_ms": round(kernel_ms, 5),
+                "kernel_timing": timing_note(args.event_every, args.steps),
                 "kernel_ms_by_rank": kernel_by_rank,
                 "bytes_per_launch": per_gpu,
                 "pmc": pmc or None,
@@ -956,6 +957,16 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
         return {"ran": False, "error": f"{type(exc).__name__}: {str(exc)[:300]}"}
     finally:
         shutil.rmtree(work, ignore_errors=True)
+
+
+def timing_note(every, steps):
+    """How `kernel_ms` was measured (mvg_engine_kernel_timing): one event pair spanning the timed
+    GEMVs, or events bracketing every Nth one."""
+    if every == -1:
+        return (f"span: one HIP event pair from the first timed GEMV's start to the stream's end at the closing "
+                f"sync, / {steps} launches (no marker between the launches; a span holding any other write to "
+                f"the shard is dropped)")
+    return f"events bracketing every {every}th GEMV on the engine stream, mean over the bracketed launches"
 
 
 def parse_runtime_line(text):

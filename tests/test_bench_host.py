@@ -649,3 +649,8 @@ def test_stop_children_ends_a_running_child_group():
     t.join(timeout=10)
     assert not t.is_alive() and got["r"].returncode != 0 and time.perf_counter() - t0 < 10
     assert not bench.CHILDREN
+
+
+def test_timing_note_names_the_measurement():
+    assert bench.timing_note(-1, 20).startswith("span:") and "/ 20 launches" in bench.timing_note(-1, 20)
+    assert "every 5th" in bench.timing_note(5, 20)
