@@ -152,11 +152,22 @@ def _shm_worker(rank, world, port, R, C, outq):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sh = SharedHostMatrix.create(R, C, 42, f"test_{port}", margin=0)
+        import bench
+        from matvec_mpi_multiplier_amd.hostshare import fill_threads
+
+        had = os.environ.get("MVG_THREADS")
+        sh = SharedHostMatrix.create(R, C, 42, f"test_{port}", margin=0, threads=fill_threads(world))
         assert sh is not None
+        assert os.environ.get("MVG_THREADS") == had  # the rank's fill threads were set for the fill only
         # every rank sees rank 0's synthetic matrix; each checks the rows its shard would pull
         lo, hi = rank * R // world, (rank + 1) * R // world
         np.testing.assert_array_equal(sh.array[lo:hi], oracle.synth_block(lo, hi - lo, 0, C, C, 42))
+        # the bench's host_memory record: every rank's share gathered on every rank (all_gather_object)
+        rec = bench.host_setup_record({**sh.timing, "pin_bytes": 8 * (hi - lo) * C, "pin_s": 0.001}, True, C)
+        assert [r["rows"] for r in rec["by_rank"]] == [R * (q + 1) // world - R * q // world for q in range(world)]
+        assert sum(r["rows"] for r in rec["by_rank"]) == R and rec["rows"] == R
+        assert all(r["threads"] == fill_threads(world) and r["fill_s"] >= 0 for r in rec["by_rank"])
+        assert rec["pin_bytes"] == 8 * R * C and rec["pin_GBps"] is not None  # (a 96 x 80 fill rounds to 0 s)
         sh.close()
         outq.put((rank, "ok"))
     finally:
@@ -166,7 +177,8 @@ def _shm_worker(rank, world, port, R, C, outq):
 @pytest.mark.parametrize("stale", [False, True])
 def test_shared_host_matrix_two_ranks(stale):
     """bench.py's end-to-end `shared` distribution: rank 0 creates the root's A in /dev/shm,
-    rank 1 maps the same bytes, both unmap, the segment is removed (no leak). A segment of the
+    rank 1 maps the same bytes, each fills its share with its share of the CPUs, both unmap, the
+    segment is removed (no leak), and the bench's per-rank setup record adds up. A segment of the
     same name left by a killed run is replaced, not fatal."""
     from multiprocessing import resource_tracker, shared_memory
 
