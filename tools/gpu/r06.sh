@@ -77,6 +77,12 @@ for l in open('$OUT/host_setup.jsonl'):
     MVG_SAME_DEVICE=1 timeout -k 30 600 python3 bench.py --gpus 4 --steps 20 --warmup 5 \
         > $OUT/bench_n4.json 2> $OUT/bench_n4.err; rc=$?
     tail -c 600 $OUT/bench_n4.json; grep "bench:" $OUT/bench_n4.err | tail -8; ok $rc || exit $rc ;;
+  rehearse2l)
+    echo "== N=2 same-device rehearsal, the driver's own launcher command, default budget"
+    MVG_SAME_DEVICE=1 timeout -k 30 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 \
+        > $OUT/bench_n2.json 2> $OUT/bench_n2.err; rc=$?
+    tail -c 600 $OUT/bench_n2.json; grep "bench:" $OUT/bench_n2.err | tail -8; ok $rc || exit $rc ;;
   rehearse8d)
     echo "== N=8 same-device rehearsal with the driver's defaults (budget 420 s; loopback sockets: the worst case)"
     MVG_SAME_DEVICE=1 timeout -k 30 700 python3 bench.py --gpus 8 --steps 20 --warmup 5 \
