@@ -184,7 +184,9 @@ def _torch_first() -> None:
     satisfies this library's dependency on libamdhip64.so.7 (same soname), so the process has one
     HIP runtime that both use, in any order, with the tree kernel's time unchanged. So when
     PyTorch is installed it is imported before the library is loaded; MVG_NO_TORCH=1 skips that
-    (a process that never uses PyTorch's GPU side then runs on /opt/rocm's runtime)."""
+    (a process that never uses PyTorch's GPU side then runs on /opt/rocm's runtime). PyTorch's
+    RCCL (librccl.so.1, 2.26.6 in this image) binds the same way, so a Python process runs the
+    library's collectives on it; runtime_info() says which copies a process runs on."""
     if os.environ.get("MVG_NO_TORCH") == "1":
         return
     try:
