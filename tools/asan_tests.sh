@@ -6,10 +6,10 @@
 # in place of the normal ones (MVG_LIB, MVG_ORACLE_LIB). Any ASan report or UBSan finding
 # aborts the run (halt_on_error, -fno-sanitize-recover). Python itself is not instrumented, so
 # the ASan runtime is preloaded; leak detection is off (the interpreter's own allocations).
-# Usage: tools/asan_tests.sh [log]   (default log: profiles/r05/asan_host_tests.log)
+# Usage: tools/asan_tests.sh [log]   (default log: profiles/r06/asan_host_tests.log)
 set -euo pipefail
 REPO="$(cd "$(dirname "$0")/.." && pwd)"
-LOG="${1:-$REPO/profiles/r05/asan_host_tests.log}"
+LOG="${1:-$REPO/profiles/r06/asan_host_tests.log}"
 mkdir -p "$(dirname "$LOG")"
 make -s -C "$REPO" asan
 RT="$(/opt/rocm/lib/llvm/bin/clang++ -print-file-name=libclang_rt.asan-x86_64.so)"
