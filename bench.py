@@ -1260,7 +1260,10 @@ def config_device(args, mm, comm, n, rank, local, distributed, barrier, budget, 
     import torch.distributed as dist
 
     name, alg, R, C = {int(c[0].split()[-1]): c for c in BASELINE_CONFIGS}[k]
-    sh = mm.plan_shard(alg, R, C, n, rank)
+    try:
+        sh = mm.plan_shard(alg, R, C, n, rank)
+    except mm.IndivisibleError as exc:  # the same on every rank: no collective is entered
+        return {"config": name, "alg": alg, "R": R, "C": C, "skipped": f"does not split over {n} GPUs: {exc}"}, None
     part = R if alg == "colwise" else sh.y_len
     need = 8 * (sh.n_rows * sh.n_cols + sh.n_cols + (9 + n) * part + R) + (1 << 30)  # + exact-mode gather buffer
     free = torch.cuda.mem_get_info(local)[0]

@@ -21,7 +21,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import ALG_BY_NAME, ALG_NAMES, SEED_A, SEED_X, Shard, XStep, check, lib, runtime_info  # noqa: F401
+from ._lib import ALG_BY_NAME, ALG_NAMES, SEED_A, SEED_X, IndivisibleError, Shard, XStep, check, lib, runtime_info  # noqa: F401
 
 
 def _alg_id(alg) -> int:

@@ -654,3 +654,15 @@ def test_stop_children_ends_a_running_child_group():
 def test_timing_note_names_the_measurement():
     assert bench.timing_note(-1, 20).startswith("span:") and "/ 20 launches" in bench.timing_note(-1, 20)
     assert "every 5th" in bench.timing_note(5, 20)
+
+
+def test_a_config_that_does_not_split_over_n_is_skipped_not_fatal():
+    """At a GPU count a config does not divide over (config 3's 65536 columns over 3 GPUs) the
+    config is recorded as skipped on every rank before any collective, as the reference prints
+    its ERROR!!! instead of running."""
+    import argparse
+
+    from matvec_mpi_multiplier_amd import multiplier as mm
+
+    entry, y = bench.config_device(argparse.Namespace(config_steps=20), mm, None, 3, 0, 0, False, None, None, None, 3)
+    assert y is None and entry["config"] == "config 3" and entry["skipped"].startswith("does not split over 3 GPUs")
