@@ -1115,16 +1115,11 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
 def host_threads():
     """The library's host thread count (csrc/host.cpp host_thread_count): $MVG_THREADS, else the
     process's CPUs capped by its cgroup quota, at most 64."""
+    from matvec_mpi_multiplier_amd.hostshare import cpu_quota
+
     if os.environ.get("MVG_THREADS"):
         return max(1, min(64, int(os.environ["MVG_THREADS"])))
-    n = len(os.sched_getaffinity(0))
-    try:
-        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max" and int(period) > 0:
-            n = min(n, max(1, -(-int(q) // int(period))))
-    except (OSError, ValueError):
-        pass
-    return max(1, min(64, n))
+    return cpu_quota()
 
 
 def loader_section(R, C):

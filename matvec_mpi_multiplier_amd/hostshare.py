@@ -52,10 +52,10 @@ def device_numa_cpus(device: int) -> set[int] | None:
         return None
 
 
-def fill_threads(local_ranks: int) -> int:
-    """Fill threads per rank when `local_ranks` ranks share this node's CPUs: the process's CPU
-    quota (cgroup cpu.max, affinity) split evenly, at least 1. Without the split every rank
-    starts the whole quota's worth of threads, and N ranks oversubscribe the quota N times."""
+def cpu_quota() -> int:
+    """The CPUs this process may run on: its affinity mask, capped by its cgroup's CPU quota
+    (cpu.max), at most 64 — the library's own host thread count without $MVG_THREADS
+    (csrc/host.cpp host_thread_count)."""
     n = len(os.sched_getaffinity(0))
     try:
         q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
@@ -63,7 +63,14 @@ def fill_threads(local_ranks: int) -> int:
             n = min(n, max(1, -(-int(q) // int(period))))
     except (OSError, ValueError):
         pass
-    return max(1, min(64, n) // max(1, local_ranks))
+    return max(1, min(64, n))
+
+
+def fill_threads(local_ranks: int) -> int:
+    """Fill threads per rank when `local_ranks` ranks share this node's CPUs: the CPU quota
+    split evenly, at least 1. Without the split every rank starts the whole quota's worth of
+    threads, and N ranks oversubscribe the quota N times."""
+    return max(1, cpu_quota() // max(1, local_ranks))
 
 
 def shm_free_bytes() -> int:
