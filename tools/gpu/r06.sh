@@ -62,6 +62,10 @@ for l in open('$OUT/host_setup.jsonl'):
       python3 tools/rocprof_by_grid.py $OUT/shapes/$1x$2 --out $OUT/shapes/kernel_by_grid_$1x$2.csv || exit $?
       head -3 $OUT/shapes/kernel_by_grid_$1x$2.csv
     done ;;
+  sliceprobe)
+    echo "== config 4's single-GPU launch: whole, split, and slice by slice, beside config 2's shape"
+    timeout -k 10 180 python3 tools/probes/slice_probe.py --rounds ${SP_ROUNDS:-4} > $OUT/slice_probe.jsonl 2> $OUT/slice_probe.err; rc=$?
+    cat $OUT/slice_probe.jsonl; [ $rc -eq 0 ] || { tail $OUT/slice_probe.err; exit $rc; } ;;
   bench)
     echo "== bench N=1 (the driver's command)"
     timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; rc=$?
