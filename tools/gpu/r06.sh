@@ -64,7 +64,7 @@ for l in open('$OUT/host_setup.jsonl'):
     done ;;
   sliceprobe)
     echo "== config 4's single-GPU launch: whole, split, and slice by slice, beside config 2's shape"
-    timeout -k 10 180 python3 tools/probes/slice_probe.py --rounds ${SP_ROUNDS:-4} > $OUT/slice_probe.jsonl 2> $OUT/slice_probe.err; rc=$?
+    timeout -k 10 180 python3 tools/probes/slice_probe.py --rounds ${SP_ROUNDS:-4} --pre-gib "${SP_PRE:-}" > $OUT/slice_probe.jsonl 2> $OUT/slice_probe.err; rc=$?
     cat $OUT/slice_probe.jsonl; [ $rc -eq 0 ] || { tail $OUT/slice_probe.err; exit $rc; } ;;
   bench)
     echo "== bench N=1 (the driver's command)"

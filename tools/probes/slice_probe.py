@@ -5,7 +5,11 @@ its own for reference, all in one process, interleaved over rounds. A slice that
 than its neighbours points at where the buffer sits in HBM; every slice as fast as config 2 with
 the whole launch slower points at the launch.
 
-    python tools/probes/slice_probe.py [--M 131072] [--K 131072] [--slices 16] [--rounds 3]
+    python tools/probes/slice_probe.py [--M 131072] [--K 131072] [--slices 16] [--rounds 3] [--pre-gib 2,32,16]
+
+--pre-gib: device buffers of these sizes allocated (hipMalloc, as the engine does), written and
+freed one after another before the big A is allocated — the bench's order (the headline's shard,
+then configs 3 and 5) — to see whether the big launch's rate depends on what the device held before.
 """
 import argparse
 import json
@@ -35,15 +39,25 @@ def main():
     ap.add_argument("--K", type=int, default=131072)
     ap.add_argument("--slices", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--pre-gib", default="")
     args = ap.parse_args()
     M, K, S = args.M, args.K, args.slices
     assert M % S == 0
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
-    A = torch.empty(M * K, dtype=torch.float64, device=dev)
+    from matvec_mpi_multiplier_amd import multiplier as mm
+
+    for gib in (float(v) for v in args.pre_gib.split(",") if v.strip()):
+        rows = int(gib * 2 ** 27) // 16384
+        b = mm.DeviceBuffer(rows * 16384)
+        check(lib.mvg_synth_fill_device(b.ptr, 16384, rows, 16384, 0, 0, 16384, 7, s), "pre fill")
+        check(lib.mvg_stream_sync(s), "sync")
+        b.free()
+    dA = mm.DeviceBuffer(M * K)  # hipMalloc'd like the engine's shard, not through the caching allocator
+    a_ptr = dA.ptr
     x = torch.empty(K, dtype=torch.float64, device=dev)
     y = torch.empty(M, dtype=torch.float64, device=dev)
-    check(lib.mvg_synth_fill_device(A.data_ptr(), K, M, K, 0, 0, K, 42, s), "fill A")
+    check(lib.mvg_synth_fill_device(a_ptr, K, M, K, 0, 0, K, 42, s), "fill A")
     check(lib.mvg_synth_fill_device(x.data_ptr(), K, 1, K, 0, 0, K, 4242, s), "fill x")
     A2 = torch.empty(16384 * 16384, dtype=torch.float64, device=dev)
     x2 = torch.empty(16384, dtype=torch.float64, device=dev)
@@ -54,15 +68,15 @@ def main():
     rows = M // S
 
     def whole():
-        check(lib.mvg_gemv(A.data_ptr(), K, x.data_ptr(), y.data_ptr(), M, K, s), "gemv")
+        check(lib.mvg_gemv(a_ptr, K, x.data_ptr(), y.data_ptr(), M, K, s), "gemv")
 
     def split(n):
         r = M // n
         for i in range(n):
-            check(lib.mvg_gemv(A.data_ptr() + 8 * i * r * K, K, x.data_ptr(), y.data_ptr() + 8 * i * r, r, K, s), "g")
+            check(lib.mvg_gemv(a_ptr + 8 * i * r * K, K, x.data_ptr(), y.data_ptr() + 8 * i * r, r, K, s), "g")
 
     def one_slice(i):
-        check(lib.mvg_gemv(A.data_ptr() + 8 * i * rows * K, K, x.data_ptr(), y.data_ptr() + 8 * i * rows, rows, K, s),
+        check(lib.mvg_gemv(a_ptr + 8 * i * rows * K, K, x.data_ptr(), y.data_ptr() + 8 * i * rows, rows, K, s),
               "slice")
 
     def cfg2():
