@@ -12,7 +12,6 @@ the undisturbed time.
 """
 import argparse
 import ctypes
-import glob
 import json
 import os
 import sys
@@ -25,15 +24,15 @@ from matvec_mpi_multiplier_amd import multiplier as mm  # noqa: E402
 from matvec_mpi_multiplier_amd._lib import check, lib  # noqa: E402
 
 
-def sysfs_used():
-    """Bytes of VRAM in use on the first amdgpu device sysfs lists (every process, the driver's
-    view), None when unreadable."""
-    for path in sorted(glob.glob("/sys/class/drm/card*/device/mem_info_vram_used")):
-        try:
-            return int(open(path).read().strip())
-        except (OSError, ValueError):
-            continue
-    return None
+def sysfs_used(dev=0):
+    """Bytes of VRAM in use on GPU `dev` as its driver counts them (every process; sysfs of the
+    device's own PCI address — the host's other GPUs are listed too), None when unreadable."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        return int(open(f"/sys/bus/pci/devices/{bdf}/mem_info_vram_used").read().strip())
+    except (OSError, ValueError):
+        return None
 
 
 def main():
