@@ -556,6 +556,7 @@ def main():
     gc.collect()
     gc.disable()
     try:
+        vram_wait = wait_vram_cleared(local)  # VRAM a previous process freed may still be being cleared
         settled = (settle(eng, args.settle_s, args.settle_max_s, distributed, local)
                    if args.settle_s > 0 else None)
         # the W warm-up steps already run with kernel timing on, so the timing events' first use
@@ -601,6 +602,7 @@ def main():
         pmc = pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)) or {}
         report.update({
             "settle": settled,
+            "vram_wait": vram_wait,
             "value": round(value, 1),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "gflops": round(2 * R * C * args.steps / elapsed / 1e9, 1),  # whole job, 2 flops per element of A
@@ -855,6 +857,57 @@ def settle(e, min_s, max_s, distributed, local, burst=20, tol=0.01):
             return {"s": round(el, 2), "bursts": len(per), "steady": steady,
                     "first_us_per_step": round(per[0] * 1e6, 1), "last_us_per_step": round(per[-1] * 1e6, 1),
                     "trace_s_us": trace}
+
+
+def _sysfs_vram_used(local):
+    """Bytes of GPU `local`'s VRAM its kernel driver counts as used (every process on the GPU),
+    from the device's own sysfs node (its PCI address: the host's other GPUs are listed too);
+    None when unreadable."""
+    import torch
+
+    try:
+        p = torch.cuda.get_device_properties(local)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/mem_info_vram_used") as f:
+            return int(f.read().strip())
+    except (OSError, ValueError, RuntimeError):
+        return None
+
+
+def vram_pending_bytes(local):
+    """VRAM the driver still counts as used beyond what this process holds (hipMemGetInfo's
+    total - free): memory an earlier section or process freed that the kernel driver is still
+    clearing. It clears freed VRAM in the background, and while it does an HBM-bound kernel runs
+    up to 5 % slow: config 2's GEMV at 301-309 us instead of 294 for 3.9 s after a 128 GiB
+    hipFree, the sysfs count dropping back exactly when the kernel recovers
+    (profiles/r06/vram_clear/). None when sysfs does not say."""
+    import torch
+
+    used = _sysfs_vram_used(local)
+    if used is None:
+        return None
+    free, total = torch.cuda.mem_get_info(local)
+    return max(0, used - (total - free))
+
+
+def wait_vram_cleared(local, timeout_s=20.0, slack=1 << 30, poll_s=0.05):
+    """Before a timed section: wait (untimed, at most `timeout_s`) until the driver has cleared
+    the VRAM freed before it — by the previous config's engine, or by the previous process on
+    the GPU — so the section is not timed while the driver's clearing shares HBM with it. What
+    it found and how long it waited goes into the line. Not at MVG_SAME_DEVICE=1 (every rank's
+    memory is on one GPU there, so this process's view never accounts for it all)."""
+    if os.environ.get("MVG_SAME_DEVICE") == "1":
+        return None
+    t0 = time.perf_counter()
+    first = vram_pending_bytes(local)
+    if first is None:
+        return None
+    pend = first
+    while pend > slack and time.perf_counter() - t0 < timeout_s:
+        time.sleep(poll_s)
+        pend = vram_pending_bytes(local)
+    return {"pending_gib": round(first / 2 ** 30, 2), "waited_s": round(time.perf_counter() - t0, 2),
+            "left_gib": round(pend / 2 ** 30, 2)}
 
 
 def warm(e, min_launches, distributed, local, seconds=0.3):
@@ -1349,6 +1402,7 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, name, alg, 
     e = mm.Multiplier(alg, R, C, comm)
     try:
         e.fill_synth()
+        vram_wait = wait_vram_cleared(local)  # the previous config's engine was just freed
         warm(e, 3, distributed, local)
         el, kms = timed(e, args.config_steps)
         tree_by_rank = by_rank[0]
@@ -1388,6 +1442,7 @@ def one_config(args, mm, comm, n, rank, local, distributed, barrier, name, alg, 
         "kernel_frac": round(per / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if kms > 0 else None,
         "pmc": pmc_summary(sh.n_rows, sh.n_cols, kernel_name(sh)),
         "exact": exact,
+        "vram_wait": vram_wait,
     }
     if rank == 0:
         entry["reference_rows"] = reference_rows_check(name, alg, R, C, n, y, yx)

@@ -666,3 +666,32 @@ def test_a_config_that_does_not_split_over_n_is_skipped_not_fatal():
 
     entry, y = bench.config_device(argparse.Namespace(config_steps=20), mm, None, 3, 0, 0, False, None, None, None, 3)
     assert y is None and entry["config"] == "config 3" and entry["skipped"].startswith("does not split over 3 GPUs")
+
+
+def test_wait_vram_cleared_waits_for_the_drivers_clearing(monkeypatch):
+    """After a large free the driver still counts the memory as used while it clears it in the
+    background (and HBM-bound kernels run slow meanwhile); the bench waits, untimed and bounded,
+    until the driver's count is back to what this process holds (fake clock and counters)."""
+    import torch
+
+    clock = [0.0]
+    monkeypatch.setattr(bench.time, "perf_counter", lambda: clock[0])
+    monkeypatch.setattr(bench.time, "sleep", lambda s: clock.__setitem__(0, clock[0] + s))
+    monkeypatch.delenv("MVG_SAME_DEVICE", raising=False)
+    GiB = 1 << 30
+    own = 3 * GiB
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (288 * GiB - own, 288 * GiB))
+    # 128 GiB pending until t = 3.9 s, then only this process's own memory
+    monkeypatch.setattr(bench, "_sysfs_vram_used", lambda local: own + (128 * GiB if clock[0] < 3.9 else 0))
+    r = bench.wait_vram_cleared(0)
+    assert r["pending_gib"] == 128.0 and r["left_gib"] == 0.0 and 3.9 <= r["waited_s"] <= 4.0
+    assert bench.wait_vram_cleared(0)["waited_s"] == 0.0  # nothing pending: no wait
+    # never cleared: the wait is bounded
+    monkeypatch.setattr(bench, "_sysfs_vram_used", lambda local: own + 50 * GiB)
+    r = bench.wait_vram_cleared(0, timeout_s=2.0)
+    assert 2.0 <= r["waited_s"] < 2.1 and r["left_gib"] == 50.0
+    # no sysfs (or a same-device rehearsal): nothing to wait on
+    monkeypatch.setattr(bench, "_sysfs_vram_used", lambda local: None)
+    assert bench.wait_vram_cleared(0) is None
+    monkeypatch.setenv("MVG_SAME_DEVICE", "1")
+    assert bench.wait_vram_cleared(0) is None
