@@ -66,6 +66,16 @@ for l in open('$OUT/host_setup.jsonl'):
     echo "== config 4's single-GPU launch: whole, split, and slice by slice, beside config 2's shape"
     timeout -k 10 180 python3 tools/probes/slice_probe.py --rounds ${SP_ROUNDS:-4} --pre-gib "${SP_PRE:-}" > $OUT/slice_probe.jsonl 2> $OUT/slice_probe.err; rc=$?
     cat $OUT/slice_probe.jsonl; [ $rc -eq 0 ] || { tail $OUT/slice_probe.err; exit $rc; } ;;
+  bench2)
+    echo "== bench N=1 twice back to back, no CPU sections (the second starts while the first's VRAM is being cleared)"
+    for i in 1 2; do
+      timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-multi --no-loader \
+          > $OUT/bench2_$i.json 2> $OUT/bench2_$i.err; rc=$?; ok $rc || exit $rc
+      python3 -c "
+import json
+p = json.loads(open('$OUT/bench2_$i.json').read().strip().splitlines()[-1])
+print($i, p['value'], p['roofline']['frac'], p.get('vram_wait'), [(c['config'], c.get('kernel_frac'), c.get('vram_wait')) for c in p['configs']])"
+    done ;;
   bench)
     echo "== bench N=1 (the driver's command)"
     timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; rc=$?
