@@ -870,7 +870,7 @@ def _sysfs_vram_used(local):
         bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
         with open(f"/sys/bus/pci/devices/{bdf}/mem_info_vram_used") as f:
             return int(f.read().strip())
-    except (OSError, ValueError, RuntimeError):
+    except Exception:  # no such device, no sysfs node, not a ROCm build: nothing to wait on
         return None
 
 
@@ -906,6 +906,33 @@ def wait_vram_cleared(local, timeout_s=20.0, slack=1 << 30, poll_s=0.05):
     while pend > slack and time.perf_counter() - t0 < timeout_s:
         time.sleep(poll_s)
         pend = vram_pending_bytes(local)
+    return {"pending_gib": round(first / 2 ** 30, 2), "waited_s": round(time.perf_counter() - t0, 2),
+            "left_gib": round(pend / 2 ** 30, 2)}
+
+
+def wait_devices_cleared(n, local, timeout_s=20.0, slack=1 << 30, poll_s=0.05):
+    """wait_vram_cleared over GPUs 0 .. n-1 before the single-process child takes all of them:
+    the rank processes have just exited, and the driver clears what they held. Only this
+    process's own GPU holds anything of ours; on the others every counted byte is pending."""
+    if os.environ.get("MVG_SAME_DEVICE") == "1":
+        return None
+    t0 = time.perf_counter()
+
+    def pending():
+        tot = 0
+        for d in range(n):
+            v = vram_pending_bytes(d) if d == local else _sysfs_vram_used(d)
+            if v is None:
+                return None
+            tot += v
+        return tot
+
+    first = pend = pending()
+    if first is None:
+        return None
+    while pend > n * slack and time.perf_counter() - t0 < timeout_s:
+        time.sleep(poll_s)
+        pend = pending()
     return {"pending_gib": round(first / 2 ** 30, 2), "waited_s": round(time.perf_counter() - t0, 2),
             "left_gib": round(pend / 2 ** 30, 2)}
 
@@ -981,13 +1008,14 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
         iters = 50
         env.update(MVG_NGPUS=str(n), MVG_SYNTH="device", MVG_ITERS=str(iters), MVG_Y_OUT=ypath)
         cmd = [exe, str(R), str(C)]
+        cleared = wait_devices_cleared(n, int(os.environ.get("LOCAL_RANK", "0")))
         t0 = time.perf_counter()
         limit = 300.0 if budget is None else max(10.0, min(300.0, budget.left() - 5.0))
         r = run_child(cmd, limit, cwd=work, env=env)
         wall = time.perf_counter() - t0
         out = {"ran": True, "command": f"MVG_NGPUS={n} MVG_SYNTH=device MVG_ITERS={iters} "
                                       f"bin/multiplier_{args.alg} {R} {C}", "rc": r.returncode,
-               "wall_s": round(wall, 2)}
+               "wall_s": round(wall, 2), "vram_wait": cleared}
         m = re.search(r"device-resident: ([\d.]+) ms per multiply, ([\d.]+) GB/s aggregate; GEMV kernel ([\d.]+) ms",
                       r.stdout)
         if r.returncode != 0 or not m or not os.path.exists(ypath):
