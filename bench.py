@@ -1155,6 +1155,8 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
         check(lib.mvg_synth_fill_device(dA.ptr, K, M, K, 0, 0, K, 42, s), "fill A")
         for v in range(nvmax):  # vector v: seed 4242 + v
             check(lib.mvg_synth_fill_device(dX.ptr + 8 * K * v, K, 1, K, 0, 0, K, 4242 + v, s), "fill x")
+        check(lib.mvg_stream_sync(s), "sync")
+        cleared = wait_vram_cleared(local)  # the end-to-end engines before it freed up to 128 GiB
 
         def t(fn):
             fn()
@@ -1168,7 +1170,7 @@ def multi_vector_section(local, M=SHARD, K=SHARD, launches=20):
             return e0.elapsed_time(e1) / launches
 
         single = t(lambda: lib.mvg_gemv(dA.ptr, K, dX.ptr, dy.ptr, M, K, s))
-        out = {"shape": [M, K], "single_ms": round(single, 5), "nv": {}}
+        out = {"shape": [M, K], "single_ms": round(single, 5), "nv": {}, "vram_wait": cleared}
         worst = 0.0
         for nv in (2, 4, 8, 16):
             ms = t(lambda: lib.mvg_gemv_multi(dA.ptr, K, dX.ptr, K, dY.ptr, M, M, K, nv, s))
