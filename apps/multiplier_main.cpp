@@ -31,6 +31,8 @@
 //   MVG_OVERLAP=n      distribute A in n row chunks, each chunk's GEMV behind its copy
 //   MVG_DATA_DIR=dir   input directory (default ./data, matr_utils.c:45,68)
 //   MVG_ITER_LOG=path  write every timed iteration's end-to-end time (s), one per line
+//   MVG_RUNTIME_ONLY=1 print the `runtime:` line (the RCCL and HIP runtime this executable binds,
+//                      as after a device-resident run) and exit: no launcher, no device work
 // Besides the CSV it prints the device-resident time (GEMV + collective only, A resident).
 #include <errno.h>
 #include <stdint.h>
@@ -87,6 +89,14 @@ int main(int argc, char** argv) {
     // one process per GPU: RCCL's intra-node IPC on this ROCm needs the dmabuf mode (the legacy
     // IPC handles fail with hipIpcGetMemHandle: invalid argument); before the HIP runtime starts
     setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);
+    if (const char* ro = getenv("MVG_RUNTIME_ONLY"); ro && ro[0] == '1') {
+        // the RCCL and HIP runtime this executable binds, printed as the device-resident run's
+        // `runtime:` line, and nothing else: no launcher, no device work
+        int rccl_v = 0, hip_v = 0;
+        const int rc = mvg_runtime_versions(&rccl_v, &hip_v);
+        printf("runtime: RCCL %d (%s), HIP %d (%s)\n", rccl_v, mvg_runtime_path(1), hip_v, mvg_runtime_path(0));
+        return rc == MVG_OK ? 0 : 1;
+    }
     if (argc < 3) {  // the reference dereferences argv[1..2] unchecked (rowwise.c:58-59)
         fprintf(stderr, "usage: %s <n_rows> <n_cols>\n", argv[0]);
         return 1;

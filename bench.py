@@ -726,6 +726,7 @@ def main():
         # the RCCL and HIP runtime the rank sections ran on (PyTorch's bundled copies when the
         # package imported torch first, _lib._torch_first); the single-process child reports its own
         rt = runtime_info()
+        rt["executables"] = executable_runtime(args.alg)  # bin/multiplier_*: /opt/rocm's, not PyTorch's
         report["runtime"] = rt
         if rccl is not None:
             rccl["version"], rccl["path"] = rt.get("rccl_version"), rt.get("rccl_path")
@@ -1048,6 +1049,20 @@ def timing_note(every, steps):
                 f"sync, / {steps} launches (no marker between the launches; a span holding any other write to "
                 f"the shard is dropped)")
     return f"events bracketing every {every}th GEMV on the engine stream, mean over the bracketed launches"
+
+
+def executable_runtime(alg):
+    """The RCCL and HIP runtime the drop-in executables bind (MVG_RUNTIME_ONLY=1
+    bin/multiplier_<alg>: the `runtime:` line, no device work), for the line's `runtime` beside
+    the rank sections' own; None when the executable is missing or says nothing."""
+    exe = os.path.join(REPO, "bin", f"multiplier_{alg}")
+    if not os.access(exe, os.X_OK):
+        return None
+    try:
+        r = run_child([exe], 30, env={**os.environ, "MVG_RUNTIME_ONLY": "1"})
+    except Exception:
+        return None
+    return parse_runtime_line(r.stdout)
 
 
 def parse_runtime_line(text):

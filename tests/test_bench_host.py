@@ -695,3 +695,12 @@ def test_wait_vram_cleared_waits_for_the_drivers_clearing(monkeypatch):
     assert bench.wait_vram_cleared(0) is None
     monkeypatch.setenv("MVG_SAME_DEVICE", "1")
     assert bench.wait_vram_cleared(0) is None
+
+
+def test_executable_runtime_names_the_executables_rccl():
+    """The line's runtime.executables: the RCCL / HIP the drop-in executables bind (their
+    MVG_RUNTIME_ONLY=1 line: /opt/rocm's, where the Python ranks run PyTorch's), no GPU needed."""
+    r = bench.executable_runtime("rowwise")
+    if r is None:
+        pytest.skip("bin/multiplier_rowwise not built")
+    assert r["rccl_origin"] == "rocm" and r["rccl_version"].count(".") == 2 and r["hip_origin"] == "rocm"
