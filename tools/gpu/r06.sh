@@ -56,6 +56,7 @@ for l in open('$OUT/host_setup.jsonl'):
     echo "== tree kernel durations, three shapes"
     for shape in "16384 16384" "131072 131072" "65536 32768"; do
       set -- $shape
+      sleep ${SHAPES_GAP:-0}  # let the driver finish clearing the previous process's VRAM
       cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/shapes/$1x$2 -o run -- \
           python3 $ROOT/tools/exact_probe.py $1 $2 50 tree > $ROOT/$OUT/shapes_$1x$2.log 2>&1; rc=$?
       cd $ROOT; [ $rc -eq 0 ] || { tail $OUT/shapes_$1x$2.log; exit $rc; }
