@@ -891,27 +891,38 @@ def vram_pending_bytes(local):
     return max(0, used - (total - free))
 
 
-def wait_vram_cleared(local, timeout_s=20.0, slack=1 << 30, poll_s=0.05):
+_VRAM_OFFSET = {}  # per GPU: bytes sysfs counts that never clear (learned after one timeout)
+
+
+def wait_vram_cleared(local, timeout_s=10.0, slack=1 << 30, poll_s=0.05):
     """Before a timed section: wait (untimed, at most `timeout_s`) until the driver has cleared
     the VRAM freed before it — by the previous config's engine, or by the previous process on
-    the GPU — so the section is not timed while the driver's clearing shares HBM with it. What
-    it found and how long it waited goes into the line. Not at MVG_SAME_DEVICE=1 (every rank's
-    memory is on one GPU there, so this process's view never accounts for it all)."""
+    the GPU — so the section is not timed while the driver's clearing shares HBM with it (137 GB
+    clear in about 4 s). What it found and how long it waited goes into the line. A count that
+    has not moved at all by the time limit is not clearing but something sysfs counts and this
+    process's view does not: it becomes that GPU's offset, and later waits do not wait on it. Not
+    at MVG_SAME_DEVICE=1 (every rank's memory is on one GPU there, so this process's view never
+    accounts for it all)."""
     if os.environ.get("MVG_SAME_DEVICE") == "1":
         return None
     t0 = time.perf_counter()
-    first = vram_pending_bytes(local)
-    if first is None:
+    raw = vram_pending_bytes(local)
+    if raw is None:
         return None
-    pend = first
+    off = _VRAM_OFFSET.get(local, 0)
+    first = pend = max(0, raw - off)
     while pend > slack and time.perf_counter() - t0 < timeout_s:
         time.sleep(poll_s)
-        pend = vram_pending_bytes(local)
-    return {"pending_gib": round(first / 2 ** 30, 2), "waited_s": round(time.perf_counter() - t0, 2),
-            "left_gib": round(pend / 2 ** 30, 2)}
+        pend = max(0, vram_pending_bytes(local) - off)
+    out = {"pending_gib": round(first / 2 ** 30, 2), "waited_s": round(time.perf_counter() - t0, 2),
+           "left_gib": round(pend / 2 ** 30, 2)}
+    if pend > slack and abs(pend - first) <= slack:
+        _VRAM_OFFSET[local] = off + pend
+        out["offset_learned_gib"] = round((off + pend) / 2 ** 30, 2)
+    return out
 
 
-def wait_devices_cleared(n, local, timeout_s=20.0, slack=1 << 30, poll_s=0.05):
+def wait_devices_cleared(n, local, timeout_s=10.0, slack=1 << 30, poll_s=0.05):
     """wait_vram_cleared over GPUs 0 .. n-1 before the single-process child takes all of them:
     the rank processes have just exited, and the driver clears what they held. Only this
     process's own GPU holds anything of ours; on the others every counted byte is pending."""

@@ -686,10 +686,18 @@ def test_wait_vram_cleared_waits_for_the_drivers_clearing(monkeypatch):
     r = bench.wait_vram_cleared(0)
     assert r["pending_gib"] == 128.0 and r["left_gib"] == 0.0 and 3.9 <= r["waited_s"] <= 4.0
     assert bench.wait_vram_cleared(0)["waited_s"] == 0.0  # nothing pending: no wait
-    # never cleared: the wait is bounded
+    # a count that never moves is an offset, not clearing: bounded once, then not waited on
+    monkeypatch.setattr(bench, "_VRAM_OFFSET", {})
     monkeypatch.setattr(bench, "_sysfs_vram_used", lambda local: own + 50 * GiB)
     r = bench.wait_vram_cleared(0, timeout_s=2.0)
-    assert 2.0 <= r["waited_s"] < 2.1 and r["left_gib"] == 50.0
+    assert 2.0 <= r["waited_s"] < 2.1 and r["left_gib"] == 50.0 and r["offset_learned_gib"] == 50.0
+    r = bench.wait_vram_cleared(0, timeout_s=2.0)
+    assert r["waited_s"] == 0.0 and r["pending_gib"] == 0.0
+    # clearing on top of the offset is still waited for
+    t_free = clock[0]
+    monkeypatch.setattr(bench, "_sysfs_vram_used", lambda local: own + 50 * GiB + (16 * GiB if clock[0] < t_free + 0.5 else 0))
+    r = bench.wait_vram_cleared(0, timeout_s=2.0)
+    assert r["pending_gib"] == 16.0 and 0.5 <= r["waited_s"] < 0.6 and "offset_learned_gib" not in r
     # no sysfs (or a same-device rehearsal): nothing to wait on
     monkeypatch.setattr(bench, "_sysfs_vram_used", lambda local: None)
     assert bench.wait_vram_cleared(0) is None
