@@ -998,7 +998,6 @@ def single_process_section(args, n, R, C, caller_nccl=None, exe=None, budget=Non
     warning of the line (main)."""
     import re
     import shutil
-    import subprocess
     import tempfile
 
     why = single_process_blocker(n)
